@@ -1,0 +1,176 @@
+"""ctypes wrapper of the CPU oracle (oracle/tcmp_oracle.c).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, tests/golden/gen_golden.py,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg -- never by the product package.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+class RrtCfg(ctypes.Structure):
+    _fields_ = [
+        ("start", ctypes.c_double * 7), ("goal", ctypes.c_double * 7),
+        ("max_samples", ctypes.c_long), ("batch", ctypes.c_int), ("torque_mode", ctypes.c_int),
+        ("mass", ctypes.c_double), ("exec_time", ctypes.c_double), ("radius", ctypes.c_double),
+        ("goal_prob", ctypes.c_double), ("goal_tol", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("replay_random", _dp), ("n_replay_random", ctypes.c_long),
+        ("replay_uniform", _dp), ("n_replay_uniform", ctypes.c_long),
+        ("obs", _dp), ("n_obs", ctypes.c_int), ("cull", ctypes.c_int), ("validate", ctypes.c_int),
+    ]
+
+
+class RrtResult(ctypes.Structure):
+    _fields_ = [("status", ctypes.c_int)] + [(n, ctypes.c_long) for n in (
+        "n_nodes", "n_samples", "edge_steps", "goal_node", "n_waypoints", "n_traj", "first_fail",
+        "n_rewires")]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_rne.argtypes = [_dp, _dp, _dp, ctypes.c_double, _dp]
+        L.orc_rne_batch.argtypes = [_dp, _dp, _dp, ctypes.c_long, ctypes.c_double, _dp]
+        L.orc_torque_ok.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_double]
+        L.orc_minjerk.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp]
+        L.orc_fk_links.argtypes = [_dp, _dp]
+        L.orc_collision.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int]
+        L.orc_pair_pd.argtypes = [ctypes.c_int, _dp, _dp]
+        L.orc_pair_pd.restype = ctypes.c_double
+        L.orc_check_edge.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                     ctypes.c_int, _ip, _dp]
+        L.orc_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _dp]
+        L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
+                                  ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
+        assert L.orc_sizeof_cfg() == ctypes.sizeof(RrtCfg), "oracle cfg layout mismatch"
+        assert L.orc_sizeof_result() == ctypes.sizeof(RrtResult), "oracle result layout mismatch"
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(_dp)
+
+
+def _arr(x, shape=None):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if shape is not None:
+        a = a.reshape(shape)
+    return a
+
+
+def rne(q, qd, qdd, payload_mass=0.0):
+    q = _arr(q, (-1, 7)); qd = _arr(qd, (-1, 7)); qdd = _arr(qdd, (-1, 7))
+    tau = np.zeros_like(q)
+    lib().orc_rne_batch(_d(q), _d(qd), _d(qdd), len(q), float(payload_mass), _d(tau))
+    return tau
+
+
+def torque_ok(q, mode, mass, qd=None, qdd=None):
+    q = _arr(q, (7,))
+    a = _arr(qd, (7,)) if qd is not None else None
+    b = _arr(qdd, (7,)) if qdd is not None else None
+    return bool(lib().orc_torque_ok(_d(q), _d(a) if a is not None else None,
+                                    _d(b) if b is not None else None, int(mode), float(mass)))
+
+
+def minjerk(waypoints, ni):
+    P = _arr(waypoints, (-1, 7))
+    K = (len(P) - 1) * ni
+    q = np.zeros((max(K, 0), 7)); qd = np.zeros_like(q); qdd = np.zeros_like(q)
+    rc = lib().orc_minjerk(_d(P), len(P), int(ni), _d(q), _d(qd), _d(qdd))
+    if rc != 0:
+        raise AssertionError("Invalid number of intervals chosen (must be greater than 0)")
+    return q, qd, qdd
+
+
+def fk_links(q):
+    q = _arr(q, (7,))
+    out = np.zeros((10, 12))
+    lib().orc_fk_links(_d(q), _d(out))
+    return out
+
+
+def obstacles_array(obs):
+    if obs is None or len(obs) == 0:
+        return np.zeros((0, 15))
+    return _arr(obs, (-1, 15))
+
+
+def collision(q, obs, cull=1):
+    q = _arr(q, (7,))
+    o = obstacles_array(obs)
+    return bool(lib().orc_collision(_d(q), _d(o) if len(o) else None, len(o), int(cull)))
+
+
+def pair_pd(link, q, box):
+    q = _arr(q, (7,)); b = _arr(box, (15,))
+    return lib().orc_pair_pd(int(link), _d(q), _d(b))
+
+
+def check_edge(q1, q2, obs, torque_mode, mass, cull=1):
+    q1 = _arr(q1, (7,)); q2 = _arr(q2, (7,)); o = obstacles_array(obs)
+    ns = ctypes.c_int(0)
+    last = np.zeros(7)
+    s = lib().orc_check_edge(_d(q1), _d(q2), _d(o) if len(o) else None, len(o),
+                             int(torque_mode), float(mass), int(cull), ctypes.byref(ns), _d(last))
+    return s, ns.value, last
+
+
+def philox_uniforms(seed, k):
+    u = np.zeros(8)
+    lib().orc_philox_uniforms(int(seed), int(k), _d(u))
+    return u
+
+
+def rrt_run(start, goal, max_samples, obs=None, torque_mode=0, mass=0.0, exec_time=5.0,
+            batch=1, seed=0, replay_random=None, replay_uniform=None, radius=0.01,
+            goal_prob=0.2, goal_tol=1e-2, cull=1, validate=True, cap_wp=1 << 16,
+            cap_traj=1 << 20):
+    """Runs the restated RRT*; returns dict with status, counters, waypoints, traj."""
+    cfg = RrtCfg()
+    cfg.start[:] = list(map(float, start)); cfg.goal[:] = list(map(float, goal))
+    cfg.max_samples = int(max_samples); cfg.batch = int(batch); cfg.torque_mode = int(torque_mode)
+    cfg.mass = float(mass); cfg.exec_time = float(exec_time); cfg.radius = float(radius)
+    cfg.goal_prob = float(goal_prob); cfg.goal_tol = float(goal_tol); cfg.seed = int(seed)
+    keep = []
+    if replay_random is not None:
+        rr = _arr(replay_random); keep.append(rr)
+        cfg.replay_random = _d(rr); cfg.n_replay_random = len(rr)
+    if replay_uniform is not None:
+        ru = _arr(replay_uniform, (-1, 7)); keep.append(ru)
+        cfg.replay_uniform = _d(ru); cfg.n_replay_uniform = len(ru)
+    o = obstacles_array(obs); keep.append(o)
+    cfg.obs = _d(o) if len(o) else None
+    cfg.n_obs = len(o); cfg.cull = int(cull); cfg.validate = int(bool(validate))
+    res = RrtResult()
+    wp = np.zeros((cap_wp, 7))
+    tq = np.zeros((cap_traj, 7)); tqd = np.zeros_like(tq); tqdd = np.zeros_like(tq)
+    psg = np.zeros(cap_traj)
+    lib().orc_rrt_run(ctypes.byref(cfg), ctypes.byref(res), _d(wp), cap_wp, _d(tq), _d(tqd),
+                      _d(tqdd), _d(psg), cap_traj)
+    out = {f: getattr(res, f) for f, _ in RrtResult._fields_}
+    W = res.n_waypoints
+    K = res.n_traj
+    out["waypoints"] = wp[:W].copy()
+    out["q"] = tq[:K].copy(); out["qd"] = tqd[:K].copy(); out["qdd"] = tqdd[:K].copy()
+    out["psg"] = psg[:K].copy()
+    return out

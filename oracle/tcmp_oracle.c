@@ -1,0 +1,865 @@
+/*
+ * tcmp_oracle.c -- CPU restatement of the reference's torque-constrained RRT* hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the checker for the HIP engine: only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it.  The product path
+ * (libtcmp.so) never links, loads or calls it.
+ *
+ * Reference: HIRO-group/torque_constrained_motion_planning @ v0 (/root/reference/src).
+ * Every function cites the reference file:line it restates.  Pinning:
+ *   - rne / torque tests / min-jerk / RRT* loop: pinned against golden vectors produced by
+ *     importing the reference Python (tests/golden/gen_golden.py -> tests/golden/ npz files).
+ *   - collision: the reference calls pybullet getClosestPoints (utils.py:2833-2849), which
+ *     is absent from this image.  The semantics restated here (a moving link's convex hull
+ *     penetrates an obstacle by >= 0.04 m, utils.py:2781 MAX_DISTANCE, distance=-0.04) are
+ *     PARITY UNPINNED against Bullet; this oracle is the reference for the GPU kernels.
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off).  Arithmetic is fp64 like numpy.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "../torque_constrained_motion_planning_amd/csrc/panda_geometry.inc"
+
+#define ORC_API __attribute__((visibility("default")))
+
+/* ------------------------------------------------------------------------------------ */
+/* Robot constants                                                                       */
+/* ------------------------------------------------------------------------------------ */
+/* joint limits / efforts: panda_mod.urdf:127,153,179,205,231,257,283 */
+static const double ORC_LO[7] = {-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973};
+static const double ORC_HI[7] = {2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973};
+static const double ORC_EFFORT[7] = {87.0, 87.0, 87.0, 87.0, 12.0, 12.0, 12.0};
+
+/* modified DH rows (a, d, alpha): rne.py:47-54 (theta = q_i, row 7 theta = 0) */
+static const double ORC_DH[8][3] = {
+    {0.0, 0.333, 0.0},
+    {0.0, 0.0, -M_PI / 2},
+    {0.0, 0.316, M_PI / 2},
+    {0.0825, 0.0, M_PI / 2},
+    {-0.0825, 0.384, -M_PI / 2},
+    {0.0, 0.0, M_PI / 2},
+    {0.088, 0.0, M_PI / 2},
+    {0.0, 0.107, 0.0},
+};
+
+/* inertia tensors rne.py:65-75 (ixx ixy ixz iyy iyz izz) */
+static const double ORC_INERTIA[9][6] = {
+    {7.0337e-01, -1.3900e-04, 6.7720e-03, 7.0661e-01, 1.9169e-02, 9.1170e-03},
+    {7.9620e-03, -3.9250e-03, 1.0254e-02, 2.8110e-02, 7.0400e-04, 2.5995e-02},
+    {3.7242e-02, -4.7610e-03, -1.1396e-02, 3.6155e-02, -1.2805e-02, 1.0830e-02},
+    {2.5853e-02, 7.7960e-03, -1.3320e-03, 1.9552e-02, 8.6410e-03, 2.8323e-02},
+    {3.5549e-02, -2.1170e-03, -4.0370e-03, 2.9474e-02, 2.2900e-04, 8.6270e-03},
+    {1.9640e-03, 1.0900e-04, -1.1580e-03, 4.3540e-03, 3.4100e-04, 5.4330e-03},
+    {1.2516e-02, -4.2800e-04, -1.1960e-03, 1.0027e-02, -7.4100e-04, 4.8150e-03},
+    {0.001, 0.0, 0.0, 0.001, 0.0, 0.001},
+    {0.1, 0.0, 0.0, 0.1, 0.0, 0.1},
+};
+/* centres of mass rne.py:107-118 */
+static const double ORC_COM[10][3] = {
+    {3.875e-03, 2.081e-03, -0.1750},
+    {-3.141e-03, -2.872e-02, 3.495e-03},
+    {2.7518e-02, 3.9252e-02, -6.6502e-02},
+    {-5.317e-02, 1.04419e-01, 2.7454e-02},
+    {-1.1953e-02, 4.1065e-02, -3.8437e-02},
+    {6.0149e-02, -1.4117e-02, -1.0517e-02},
+    {1.0517e-02, -4.252e-03, 6.1597e-02},
+    {0, 0, 0},
+    {0, 0, 0},
+    {0, 0, 0},
+};
+/* masses rne.py:125-136 (slot 9 = payload, set by add_payload) */
+static const double ORC_MASS[9] = {4.970684, 0.646926, 3.228604, 3.587895, 1.225946,
+                                   1.666555, 7.35522e-01, 0.0, 0.68};
+
+/* URDF joint origins for forward kinematics of the collision links (pybullet uses these):
+ * panda_mod.urdf joint1..joint7 origins (:122,148,174,200,226,252,278), joint8 (:291),
+ * hand joint rpy (:10), finger joints (:65,72), finger open width 0.04
+ * (panda_primitives.py:320-322 sets fingers to their upper limit). */
+static const double ORC_J_XYZ[7][3] = {
+    {0, 0, 0.333}, {0, 0, 0}, {0, -0.316, 0}, {0.0825, 0, 0},
+    {-0.0825, 0.384, 0}, {0, 0, 0}, {0.088, 0, 0}};
+static const double ORC_J_ROLL[7] = {0.0, -1.57079632679, 1.57079632679, 1.57079632679,
+                                     -1.57079632679, 1.57079632679, 1.57079632679};
+#define ORC_FLANGE_Z 0.107
+#define ORC_HAND_YAW (-0.785398163397)
+#define ORC_FINGER_Z 0.0584
+#define ORC_FINGER_OPEN 0.04
+
+/* collision threshold: utils.py:2781 MAX_DISTANCE=0.04 used as distance=-MAX_DISTANCE
+ * in get_closest_points (utils.py:2833) -> colliding iff penetration >= 0.04 */
+#define ORC_PEN 0.04
+
+/* ------------------------------------------------------------------------------------ */
+/* rne.py restated with 6x6 spatial algebra (rne.py:4-27, 32-63, 181-254)               */
+/* ------------------------------------------------------------------------------------ */
+static void skew3(const double v[3], double S[3][3]) { /* rne.py:4-7 */
+  S[0][0] = 0; S[0][1] = -v[2]; S[0][2] = v[1];
+  S[1][0] = v[2]; S[1][1] = 0; S[1][2] = -v[0];
+  S[2][0] = -v[1]; S[2][1] = v[0]; S[2][2] = 0;
+}
+
+static void tf_mat(double a, double d, double alpha, double q, double T[4][4]) { /* rne.py:32-44 */
+  T[0][0] = cos(q); T[0][1] = -sin(q); T[0][2] = 0; T[0][3] = a;
+  T[1][0] = sin(q) * cos(alpha); T[1][1] = cos(q) * cos(alpha); T[1][2] = -sin(alpha);
+  T[1][3] = -sin(alpha) * d;
+  T[2][0] = sin(q) * sin(alpha); T[2][1] = cos(q) * sin(alpha); T[2][2] = cos(alpha);
+  T[2][3] = cos(alpha) * d;
+  T[3][0] = 0; T[3][1] = 0; T[3][2] = 0; T[3][3] = 1;
+}
+
+/* get_parent_to_child_transform(q, i-1, i) (rne.py:46-63): inv(DH_i) for i<=8, I for i>8.
+ * The reference inverts with np.linalg.inv; the rigid inverse [R^T, -R^T p] is the same
+ * matrix up to rounding. */
+static void xup_of(const double q10[10], int i, double X[4][4]) {
+  int row = i - 1;
+  if (row < 8) {
+    double T[4][4];
+    tf_mat(ORC_DH[row][0], ORC_DH[row][1], ORC_DH[row][2], row < 7 ? q10[row] : 0.0, T);
+    for (int r = 0; r < 3; ++r) {
+      for (int c = 0; c < 3; ++c) X[r][c] = T[c][r];
+      X[r][3] = -(T[0][r] * T[0][3] + T[1][r] * T[1][3] + T[2][r] * T[2][3]);
+    }
+    X[3][0] = X[3][1] = X[3][2] = 0; X[3][3] = 1;
+  } else {
+    memset(X, 0, sizeof(double) * 16);
+    X[0][0] = X[1][1] = X[2][2] = X[3][3] = 1;
+  }
+  if (i == 7) X[2][3] = 0; /* rne.py:226-227 */
+}
+
+static void adjoint(const double X[4][4], double A[6][6]) { /* rne.py:9-14 */
+  double S[3][3], t[3] = {X[0][3], X[1][3], X[2][3]};
+  skew3(t, S);
+  memset(A, 0, sizeof(double) * 36);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      A[r][c] = X[r][c];
+      A[r + 3][c + 3] = X[r][c];
+      double s = 0;
+      for (int k = 0; k < 3; ++k) s += S[r][k] * X[k][c];
+      A[r][c + 3] = s;
+    }
+}
+
+static void spatial_inertia(double m, const double c[3], const double I[3][3], double M[6][6]) {
+  /* rne.py:16-19 */
+  double C[3][3];
+  skew3(c, C);
+  for (int r = 0; r < 3; ++r)
+    for (int k = 0; k < 3; ++k) {
+      M[r][k] = (r == k) ? m : 0.0;
+      M[r][k + 3] = m * C[k][r];
+      M[r + 3][k] = m * C[r][k];
+      double s = 0;
+      for (int j = 0; j < 3; ++j) s += C[r][j] * C[k][j];
+      M[r + 3][k + 3] = I[r][k] + m * s;
+    }
+}
+
+static void crm(const double v[6], double M[6][6]) { /* rne.py:21-24 */
+  double W[3][3], V[3][3];
+  skew3(v + 3, W);
+  skew3(v, V);
+  memset(M, 0, sizeof(double) * 36);
+  for (int r = 0; r < 3; ++r)
+    for (int c = 0; c < 3; ++c) {
+      M[r][c] = W[r][c];
+      M[r][c + 3] = V[r][c];
+      M[r + 3][c + 3] = W[r][c];
+    }
+}
+
+static void mv6(const double M[6][6], const double v[6], double o[6]) {
+  for (int r = 0; r < 6; ++r) {
+    double s = 0;
+    for (int k = 0; k < 6; ++k) s += M[r][k] * v[k];
+    o[r] = s;
+  }
+}
+static void mtv6(const double M[6][6], const double v[6], double o[6]) {
+  for (int r = 0; r < 6; ++r) {
+    double s = 0;
+    for (int k = 0; k < 6; ++k) s += M[k][r] * v[k];
+    o[r] = s;
+  }
+}
+
+/* rne(q, qd, qdd) with the module-level payload state (rne.py:171-195) made explicit:
+ * payload present iff payload_mass > 0 (add_payload's `if m > 0`, rne.py:184). */
+ORC_API void orc_rne(const double* q7, const double* qd7, const double* qdd7, double payload_mass,
+                     double* tau7) {
+  double q[10] = {0}, qd[10] = {0}, qdd[10] = {0};
+  for (int i = 0; i < 7; ++i) { q[i] = q7[i]; qd[i] = qd7[i]; qdd[i] = qdd7[i]; }
+  int has_payload = payload_mass > 0;
+  int nb = 9 + has_payload;
+  double v[10][6], a[10][6], f[10][6], Ad[10][6][6];
+  for (int i = 1; i <= nb; ++i) {
+    int p = i - 1;
+    double X[4][4];
+    xup_of(q, i, X);
+    adjoint(X, Ad[p]);
+    double vJ[6] = {0, 0, 0, 0, 0, qd[p]};
+    if (i == 1) {
+      double g[6] = {0, 0, 9.81, 0, 0, 0}; /* -a_grav, rne.py:199,232 */
+      for (int k = 0; k < 6; ++k) v[p][k] = vJ[k];
+      mv6(Ad[p], g, a[p]);
+      a[p][5] += qdd[p];
+    } else {
+      double t[6], cm[6][6], t2[6];
+      mv6(Ad[p], v[p - 1], t);
+      for (int k = 0; k < 6; ++k) v[p][k] = t[k] + vJ[k];
+      mv6(Ad[p], a[p - 1], t);
+      crm(v[p], cm);
+      mv6(cm, vJ, t2);
+      for (int k = 0; k < 6; ++k) a[p][k] = t[k] + t2[k];
+      a[p][5] += qdd[p];
+    }
+    /* spatial inertia of body p (rne.py:240) */
+    double m, I3[3][3], M[6][6];
+    if (p < 9) {
+      m = ORC_MASS[p];
+      const double* n = ORC_INERTIA[p];
+      double tmp[3][3] = {{n[0], n[1], n[2]}, {n[1], n[3], n[4]}, {n[2], n[4], n[5]}};
+      memcpy(I3, tmp, sizeof(tmp));
+    } else {
+      /* payload: mass m, COM 0, inertia new_inertia([0,0,0.14+0.025], m) (rne.py:85-100,181-188) */
+      m = payload_mass;
+      double r2 = 0.165;
+      double tmp[3][3] = {{m * (0.0 + r2 * r2), -m * 0.0, -m * 0.0},
+                          {-m * 0.0, m * (0.0 + r2 * r2), -m * 0.0},
+                          {-m * 0.0, -m * 0.0, m * (0.0 + 0.0)}};
+      memcpy(I3, tmp, sizeof(tmp));
+    }
+    spatial_inertia(m, ORC_COM[p], I3, M);
+    double Ia[6], Iv[6], cf[6][6], cfIv[6];
+    mv6(M, a[p], Ia);
+    mv6(M, v[p], Iv);
+    crm(v[p], cf); /* crf = -crm^T (rne.py:26-27) */
+    mtv6(cf, Iv, cfIv);
+    for (int k = 0; k < 6; ++k) f[p][k] = Ia[k] - cfIv[k];
+  }
+  double tau[10];
+  for (int i = nb; i >= 1; --i) { /* rne.py:247-251 */
+    int p = i - 1;
+    tau[p] = f[p][5];
+    if (i != 1) {
+      double t[6];
+      mtv6(Ad[p], f[p], t);
+      for (int k = 0; k < 6; ++k) f[p - 1][k] += t[k];
+    }
+  }
+  for (int i = 0; i < 7; ++i) tau7[i] = tau[i];
+}
+
+ORC_API void orc_rne_batch(const double* q, const double* qd, const double* qdd, long n,
+                           double payload_mass, double* tau) {
+  for (long i = 0; i < n; ++i) orc_rne(q + 7 * i, qd + 7 * i, qdd + 7 * i, payload_mass, tau + 7 * i);
+}
+
+/* Torque tests.  mode 0 = base (panda_primitives.py:13-16, always True);
+ * 1 = nov (:118-153: RNE with v = a = 0 always); 2 = rne (:155-193: RNE with the given
+ * v/a, zeros when None).  Payload added iff mass > 0.01 (:142-144, :178-180).
+ * Joint 7 never checked and equality fails: range(len(max_limits)-1), `>=` (:182-183). */
+ORC_API int orc_torque_ok(const double* q, const double* qd, const double* qdd, int mode,
+                          double mass) {
+  if (mode == 0) return 1;
+  double z[7] = {0}, tau[7];
+  const double* v = (mode == 2 && qd) ? qd : z;
+  const double* a = (mode == 2 && qdd) ? qdd : z;
+  orc_rne(q, v, a, mass > 0.01 ? mass : 0.0, tau);
+  for (int i = 0; i < 6; ++i)
+    if (fabs(tau[i]) >= ORC_EFFORT[i]) return 0;
+  return 1;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* min_jerk_v2.py restated                                                              */
+/* ------------------------------------------------------------------------------------ */
+/* minjerk_coefficients (min_jerk_v2.py:80-142) with unit durations; coeff[N-1][7][6] */
+static void orc_minjerk_coeffs(const double* P, int rows, double* coeff) {
+  int N = rows - 1;
+  double x[7], v[7], a[7];
+  for (int k = 0; k < 7; ++k) { x[k] = P[k]; v[k] = 0; a[k] = 0; }
+  for (int i = 0; i < N; ++i) {
+    const double t = 1.0;
+    double gx[7], gv[7];
+    for (int k = 0; k < 7; ++k) gx[k] = P[7 * (i + 1) + k];
+    if (i == N - 1) {
+      for (int k = 0; k < 7; ++k) gv[k] = 0.0;
+    } else {
+      for (int k = 0; k < 7; ++k) {
+        double d0 = P[7 * (i + 1) + k] - P[7 * i + k];
+        double d1 = P[7 * (i + 2) + k] - P[7 * (i + 1) + k];
+        double v0 = d0 / t, v1 = d1 / t;
+        gv[k] = (v0 * v1 >= 1e-10) ? 0.5 * (v0 + v1) : 0.0; /* :118 */
+      }
+    }
+    for (int k = 0; k < 7; ++k) {
+      double ga = 0.0;
+      double A = (gx[k] - (x[k] + v[k] * t + (a[k] / 2.0) * t * t)) / (t * t * t);
+      double B = (gv[k] - (v[k] + a[k] * t)) / (t * t);
+      double C = (ga - a[k]) / t;
+      double* c = coeff + (size_t)(i * 7 + k) * 6;
+      c[0] = x[k];
+      c[1] = v[k];
+      c[2] = a[k] / 2.0;
+      c[3] = 10 * A - 4 * B + 0.5 * C;
+      c[4] = (-15 * A + 7 * B - C) / t;
+      c[5] = (6 * A - 3 * B + 0.5 * C) / (t * t);
+    }
+    for (int k = 0; k < 7; ++k) { x[k] = gx[k]; v[k] = gv[k]; } /* a never updated (:132-133) */
+  }
+}
+
+/* get_dynamics_fn_v5 body (panda_primitives.py:299-316) + minjerk_trajectory (:144-182)
+ * + _minjerk_trajectory_point (:184-222).  Writes (rows-1)*ni samples. */
+ORC_API int orc_minjerk(const double* P, int rows, int ni, double* q, double* qd, double* qdd) {
+  if (ni <= 0) return -1; /* AssertionError at min_jerk_v2.py:166 */
+  int N = rows - 1;
+  double* coeff = (double*)malloc(sizeof(double) * (size_t)(N > 0 ? N : 1) * 42);
+  orc_minjerk_coeffs(P, rows, coeff);
+  double interval = 1.0 / ni;
+  double step = (ni > 1) ? (1.0 - interval) / (double)(ni - 1) : 0.0; /* np.linspace */
+  long o = 0;
+  for (int s = 0; s < N; ++s) {
+    for (int j = 0; j < ni; ++j) {
+      double t;
+      if (ni > 1) t = (j == ni - 1) ? 1.0 : ((double)j * step + interval);
+      else t = 0.0 * (1.0 - interval) + interval;
+      t = t * 1.0; /* duration_array[current_mpt] */
+      t = t * 1.0; /* tm */
+      double t2 = pow(t, 2), t3 = pow(t, 3), t4 = pow(t, 4), t5 = pow(t, 5);
+      for (int k = 0; k < 7; ++k) {
+        const double* c = coeff + (size_t)(s * 7 + k) * 6;
+        q[o * 7 + k] = c[0] + c[1] * t + c[2] * t2 + c[3] * t3 + c[4] * t4 + c[5] * t5;
+        qd[o * 7 + k] = c[1] + 2 * c[2] * t + 3 * c[3] * t2 + 4 * c[4] * t3 + 5 * c[5] * t4;
+        qdd[o * 7 + k] = 2 * c[2] + 6 * c[3] * t + 12 * c[4] * t2 + 20 * c[5] * t3;
+      }
+      ++o;
+    }
+  }
+  free(coeff);
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* utils.py closures: distance / extend / limits / sample                               */
+/* ------------------------------------------------------------------------------------ */
+/* get_distance_fn (utils.py:3010-3017): sqrt(dot(w, diff*diff)), w = 1/radius = 10 */
+static double orc_dist(const double* a, const double* b, const double* w) {
+  double s = 0;
+  for (int k = 0; k < 7; ++k) {
+    double d = b[k] - a[k];
+    s += w[k] * (d * d);
+  }
+  return sqrt(s);
+}
+
+/* get_extend_fn (utils.py:3068-3077): steps = int(norm(diff/res)); refine with steps+1 */
+static int orc_num_steps(const double* q1, const double* q2, const double* res) {
+  double s = 0;
+  for (int k = 0; k < 7; ++k) {
+    double x = (q2[k] - q1[k]) / res[k];
+    s += x * x;
+  }
+  return (int)sqrt(s) + 1;
+}
+
+/* get_refine_fn step (utils.py:3031-3041): q <- (1/(n-i)) * (q2 - q) + q */
+static void orc_refine_step(double* q, const double* q2, int n, int i) {
+  double r = 1.0 / (double)(n - i);
+  for (int k = 0; k < 7; ++k) q[k] = r * (q2[k] - q[k]) + q[k];
+}
+
+/* get_limits_fn (utils.py:3154-3163) with all_between inclusive (utils.py:1150-1154) */
+static int orc_limits_violated(const double* q) {
+  for (int k = 0; k < 7; ++k)
+    if (!(ORC_LO[k] <= q[k]) || !(q[k] <= ORC_HI[k])) return 1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Forward kinematics of the collision links (pybullet resetJointState + link frames)    */
+/* ------------------------------------------------------------------------------------ */
+typedef struct { double R[9]; double p[3]; } orc_frame;
+
+static void fr_mul(const orc_frame* A, const double R[9], const double t[3], orc_frame* O) {
+  /* O = A * [R t] */
+  orc_frame r;
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j)
+      r.R[3 * i + j] = A->R[3 * i + 0] * R[0 + j] + A->R[3 * i + 1] * R[3 + j] + A->R[3 * i + 2] * R[6 + j];
+    r.p[i] = A->R[3 * i + 0] * t[0] + A->R[3 * i + 1] * t[1] + A->R[3 * i + 2] * t[2] + A->p[i];
+  }
+  *O = r;
+}
+
+/* frames[10]: link1..link7, hand, leftfinger, rightfinger (world = robot base frame) */
+ORC_API void orc_fk_links(const double* q, double* out /* 10 x 12: R(9) p(3) */) {
+  orc_frame T, F[10];
+  memset(&T, 0, sizeof(T));
+  T.R[0] = T.R[4] = T.R[8] = 1.0;
+  for (int j = 0; j < 7; ++j) {
+    double cr = cos(ORC_J_ROLL[j]), sr = sin(ORC_J_ROLL[j]);
+    double cq = cos(q[j]), sq = sin(q[j]);
+    /* Rx(roll) * Rz(q) */
+    double R[9] = {cq, -sq, 0.0, cr * sq, cr * cq, -sr, sr * sq, sr * cq, cr};
+    fr_mul(&T, R, ORC_J_XYZ[j], &T);
+    F[j] = T;
+  }
+  double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  double tz[3] = {0, 0, ORC_FLANGE_Z};
+  orc_frame L8;
+  fr_mul(&T, I, tz, &L8);
+  double cy = cos(ORC_HAND_YAW), sy = sin(ORC_HAND_YAW);
+  double Rz[9] = {cy, -sy, 0, sy, cy, 0, 0, 0, 1};
+  double z0[3] = {0, 0, 0};
+  fr_mul(&L8, Rz, z0, &F[7]);
+  double tl[3] = {0, ORC_FINGER_OPEN, ORC_FINGER_Z}, tr[3] = {0, -ORC_FINGER_OPEN, ORC_FINGER_Z};
+  fr_mul(&F[7], I, tl, &F[8]);
+  fr_mul(&F[7], I, tr, &F[9]);
+  for (int l = 0; l < 10; ++l) {
+    memcpy(out + 12 * l, F[l].R, 9 * sizeof(double));
+    memcpy(out + 12 * l + 9, F[l].p, 3 * sizeof(double));
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Collision: moving link convex hull vs obstacle box, penetration >= 0.04               */
+/* Obstacle record (15 doubles): centre c(3), R(9, row-major, columns = box axes), half(3) */
+/* ------------------------------------------------------------------------------------ */
+/* link-frame box: centre cl, axes A (columns), half h */
+static void box_to_link(const double* fr, const double* ob, double cl[3], double A[9]) {
+  const double* R = fr;
+  const double* p = fr + 9;
+  double d[3] = {ob[0] - p[0], ob[1] - p[1], ob[2] - p[2]};
+  for (int i = 0; i < 3; ++i) cl[i] = R[0 + i] * d[0] + R[3 + i] * d[1] + R[6 + i] * d[2];
+  const double* B = ob + 3;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      A[3 * i + j] = R[0 + i] * B[0 + j] + R[3 + i] * B[3 + j] + R[6 + i] * B[6 + j];
+}
+
+/* exact penetration depth hull(link) vs box, both in the link frame: minimum overlap
+ * over the candidate separating axes of two convex polytopes (box faces, hull facets,
+ * hull-edge x box-axis).  Returns min(overlap) (negative = separated). */
+ORC_API double orc_hull_box_pd_local(int link, const double cl[3], const double A[9],
+                                     const double h[3]) {
+  const int v0 = tcmp_geo_vert_off[link], v1 = tcmp_geo_vert_off[link + 1];
+  const int f0 = tcmp_geo_plane_off[link], f1 = tcmp_geo_plane_off[link + 1];
+  const int e0 = tcmp_geo_edge_off[link], e1 = tcmp_geo_edge_off[link + 1];
+  double pd = INFINITY;
+  /* box face axes */
+  for (int i = 0; i < 3; ++i) {
+    double ax[3] = {A[0 + i], A[3 + i], A[6 + i]};
+    double mn = INFINITY, mx = -INFINITY;
+    for (int v = v0; v < v1; ++v) {
+      const double* P = tcmp_geo_verts + 4 * v;
+      double d = ax[0] * P[0] + ax[1] * P[1] + ax[2] * P[2];
+      mn = fmin(mn, d);
+      mx = fmax(mx, d);
+    }
+    double pc = ax[0] * cl[0] + ax[1] * cl[1] + ax[2] * cl[2];
+    double ov = fmin(mx - (pc - h[i]), (pc + h[i]) - mn);
+    pd = fmin(pd, ov);
+  }
+  /* hull facet axes */
+  for (int f = f0; f < f1; ++f) {
+    const double* P = tcmp_geo_planes + 8 * f;
+    double pc = P[0] * cl[0] + P[1] * cl[1] + P[2] * cl[2];
+    double rad = 0;
+    for (int i = 0; i < 3; ++i) rad += h[i] * fabs(P[0] * A[0 + i] + P[1] * A[3 + i] + P[2] * A[6 + i]);
+    double ov = fmin(P[3] - (pc - rad), (pc + rad) - P[4]);
+    pd = fmin(pd, ov);
+  }
+  /* hull edge x box axis */
+  for (int e = e0; e < e1; ++e) {
+    const double* E = tcmp_geo_edges + 4 * e;
+    for (int i = 0; i < 3; ++i) {
+      double ax[3] = {A[0 + i], A[3 + i], A[6 + i]};
+      double n[3] = {E[1] * ax[2] - E[2] * ax[1], E[2] * ax[0] - E[0] * ax[2],
+                     E[0] * ax[1] - E[1] * ax[0]};
+      double len2 = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+      if (len2 < 1e-12) continue;
+      double mn = INFINITY, mx = -INFINITY;
+      for (int v = v0; v < v1; ++v) {
+        const double* P = tcmp_geo_verts + 4 * v;
+        double d = n[0] * P[0] + n[1] * P[1] + n[2] * P[2];
+        mn = fmin(mn, d);
+        mx = fmax(mx, d);
+      }
+      double pc = n[0] * cl[0] + n[1] * cl[1] + n[2] * cl[2];
+      double rad = 0;
+      for (int j = 0; j < 3; ++j) rad += h[j] * fabs(n[0] * A[0 + j] + n[1] * A[3 + j] + n[2] * A[6 + j]);
+      double ov = fmin(mx - (pc - rad), (pc + rad) - mn) / sqrt(len2);
+      pd = fmin(pd, ov);
+    }
+  }
+  return pd;
+}
+
+/* penetration depth of two oriented boxes (15-axis SAT, exact for box-box).
+ * boxes given in one frame: centre c, axes (columns of 3x3 row-major), half */
+static double obb_obb_pd(const double ca[3], const double Aa[9], const double ha[3],
+                         const double cb[3], const double Ab[9], const double hb[3]) {
+  double axes[15][3];
+  int na = 0;
+  for (int i = 0; i < 3; ++i) { axes[na][0] = Aa[i]; axes[na][1] = Aa[3 + i]; axes[na][2] = Aa[6 + i]; ++na; }
+  for (int i = 0; i < 3; ++i) { axes[na][0] = Ab[i]; axes[na][1] = Ab[3 + i]; axes[na][2] = Ab[6 + i]; ++na; }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double a[3] = {Aa[i], Aa[3 + i], Aa[6 + i]}, b[3] = {Ab[j], Ab[3 + j], Ab[6 + j]};
+      axes[na][0] = a[1] * b[2] - a[2] * b[1];
+      axes[na][1] = a[2] * b[0] - a[0] * b[2];
+      axes[na][2] = a[0] * b[1] - a[1] * b[0];
+      ++na;
+    }
+  double d[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+  double pd = INFINITY;
+  for (int k = 0; k < 15; ++k) {
+    const double* n = axes[k];
+    double len2 = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+    if (len2 < 1e-12) continue;
+    double ra = 0, rb = 0;
+    for (int i = 0; i < 3; ++i) {
+      ra += ha[i] * fabs(n[0] * Aa[i] + n[1] * Aa[3 + i] + n[2] * Aa[6 + i]);
+      rb += hb[i] * fabs(n[0] * Ab[i] + n[1] * Ab[3 + i] + n[2] * Ab[6 + i]);
+    }
+    double dist = fabs(n[0] * d[0] + n[1] * d[1] + n[2] * d[2]);
+    double ov = (ra + rb - dist) / sqrt(len2);
+    pd = fmin(pd, ov);
+  }
+  return pd;
+}
+
+/* pair classification.  Returns 1 if link hull penetrates obstacle by >= 0.04.
+ * cull=1 uses the conservative outer-OBB (free) and inner-box (collision) bounds first;
+ * cull=0 always runs the exact hull test.  Both give the same answer. */
+static int orc_pair_collides(int link, const double* fr, const double* ob, int cull, long* n_exact) {
+  double cl[3], A[9];
+  box_to_link(fr, ob, cl, A);
+  const double* h = ob + 12;
+  if (cull) {
+    const double* bx = tcmp_geo_boxes + 18 * link;
+    const double* oc = bx;
+    const double* oR = bx + 3;
+    const double* oh = bx + 12;
+    const double* ih = bx + 15;
+    if (obb_obb_pd(oc, oR, oh, cl, A, h) < ORC_PEN) return 0;
+    if ((ih[0] > 0) && obb_obb_pd(oc, oR, ih, cl, A, h) >= ORC_PEN) return 1;
+  }
+  if (n_exact) ++*n_exact;
+  return orc_hull_box_pd_local(link, cl, A, h) >= ORC_PEN;
+}
+
+ORC_API double orc_pair_pd(int link, const double* q, const double* ob) {
+  double fr[120], cl[3], A[9];
+  orc_fk_links(q, fr);
+  box_to_link(fr + 12 * link, ob, cl, A);
+  return orc_hull_box_pd_local(link, cl, A, ob + 12);
+}
+
+/* collision_fn (utils.py:3165-3218): limits first, then every moving link x obstacle.
+ * Self-collision off (utils.py:56 SELF_COLLISIONS=False), no attachments. */
+ORC_API int orc_collision(const double* q, const double* obs, int n_obs, int cull) {
+  if (orc_limits_violated(q)) return 1;
+  if (n_obs <= 0) return 0;
+  double fr[120];
+  orc_fk_links(q, fr);
+  for (int l = 0; l < TCMP_NLINKS; ++l)
+    for (int o = 0; o < n_obs; ++o)
+      if (orc_pair_collides(l, fr + 12 * l, obs + 15 * o, cull, 0)) return 1;
+  return 0;
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* safe_path_force_aware over extend(q1, q2) (rrt_star.py:90-98)                         */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  const double* obs;
+  int n_obs;
+  int torque_mode;
+  double mass;
+  int cull;
+  double res[7];
+  double w[7];
+  long edge_steps; /* statistics */
+} orc_ctx;
+
+static int orc_edge(orc_ctx* C, const double* q1, const double* q2, int* nsteps, double* last) {
+  int n = orc_num_steps(q1, q2, C->res);
+  double q[7];
+  memcpy(q, q1, sizeof(q));
+  int safe = 0;
+  for (int i = 0; i < n; ++i) {
+    double qn[7];
+    memcpy(qn, q, sizeof(qn));
+    orc_refine_step(qn, q2, n, i);
+    C->edge_steps++;
+    if (orc_collision(qn, C->obs, C->n_obs, C->cull)) break;
+    if (!orc_torque_ok(qn, 0, 0, C->torque_mode, C->mass)) break;
+    memcpy(q, qn, sizeof(q));
+    ++safe;
+  }
+  *nsteps = n;
+  if (safe > 0) memcpy(last, q, sizeof(q));
+  return safe;
+}
+
+ORC_API int orc_check_edge(const double* q1, const double* q2, const double* obs, int n_obs,
+                           int torque_mode, double mass, int cull, int* nsteps, double* last) {
+  orc_ctx C;
+  memset(&C, 0, sizeof(C));
+  C.obs = obs; C.n_obs = n_obs; C.torque_mode = torque_mode; C.mass = mass; C.cull = cull;
+  for (int k = 0; k < 7; ++k) { C.res[k] = 0.1; C.w[k] = 10.0; }
+  return orc_edge(&C, q1, q2, nsteps, last);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Philox4x32-10 sample stream (engine's batched sampler; same definition as the GPU)    */
+/* ------------------------------------------------------------------------------------ */
+static void philox(uint32_t c[4], uint32_t k0, uint32_t k1) {
+  for (int r = 0; r < 10; ++r) {
+    uint64_t p0 = (uint64_t)0xD2511F53u * c[0];
+    uint64_t p1 = (uint64_t)0xCD9E8D57u * c[2];
+    uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+    uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+    uint32_t n0 = hi1 ^ c[1] ^ k0, n2 = hi0 ^ c[3] ^ k1;
+    c[0] = n0; c[1] = lo1; c[2] = n2; c[3] = lo0;
+    k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+  }
+}
+/* 8 uniforms in [0,1) for sample index k: u[0..6] configuration, u[7] goal-bias draw */
+ORC_API void orc_philox_uniforms(uint64_t seed, uint64_t k, double* u) {
+  for (int j = 0; j < 4; ++j) {
+    uint32_t c[4] = {(uint32_t)k, (uint32_t)(k >> 32), (uint32_t)j, 0x7463u};
+    philox(c, (uint32_t)seed, (uint32_t)(seed >> 32));
+    uint64_t a = ((uint64_t)c[0] << 32) | c[1], b = ((uint64_t)c[2] << 32) | c[3];
+    u[2 * j] = (double)(a >> 11) * 0x1.0p-53;
+    u[2 * j + 1] = (double)(b >> 11) * 0x1.0p-53;
+  }
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* rrt_star_force_aware (rrt_star.py:151-211), generalised to B candidates per round.     */
+/* B = 1 is exactly the reference's sequential loop.                                     */
+/* ------------------------------------------------------------------------------------ */
+typedef struct {
+  double start[7], goal[7];
+  long max_samples;
+  int batch;
+  int torque_mode;
+  double mass;
+  double exec_time;
+  double radius;
+  double goal_prob;
+  double goal_tol;
+  uint64_t seed;
+  const double* replay_random; long n_replay_random;
+  const double* replay_uniform; long n_replay_uniform; /* 7 doubles per draw */
+  const double* obs; int n_obs;
+  int cull;
+  int validate;
+} orc_rrt_cfg;
+
+typedef struct {
+  int status; /* 0 ok, 1 start/goal collision, 2 no goal, 3 validation failed, 4 minjerk assert,
+                 5 replay stream exhausted, 6 capacity */
+  long n_nodes, n_samples, edge_steps, goal_node, n_waypoints, n_traj, first_fail;
+  long n_rewires;
+} orc_rrt_result;
+
+typedef struct {
+  double* cfg;   /* 7 */
+  double* cost;
+  int* parent;
+  double* tgt;   /* 7 */
+  int* nsteps;
+  int* nsafe;
+  long n, cap;
+} orc_tree;
+
+static void tree_push(orc_tree* t, const double* c, double cost, int parent, const double* tgt,
+                      int ns, int nsafe) {
+  if (t->n == t->cap) {
+    t->cap = t->cap ? 2 * t->cap : 1024;
+    t->cfg = realloc(t->cfg, sizeof(double) * 7 * t->cap);
+    t->cost = realloc(t->cost, sizeof(double) * t->cap);
+    t->parent = realloc(t->parent, sizeof(int) * t->cap);
+    t->tgt = realloc(t->tgt, sizeof(double) * 7 * t->cap);
+    t->nsteps = realloc(t->nsteps, sizeof(int) * t->cap);
+    t->nsafe = realloc(t->nsafe, sizeof(int) * t->cap);
+  }
+  long i = t->n++;
+  memcpy(t->cfg + 7 * i, c, 7 * sizeof(double));
+  t->cost[i] = cost;
+  t->parent[i] = parent;
+  if (tgt) memcpy(t->tgt + 7 * i, tgt, 7 * sizeof(double));
+  else memcpy(t->tgt + 7 * i, c, 7 * sizeof(double));
+  t->nsteps[i] = ns;
+  t->nsafe[i] = nsafe;
+}
+
+static void tree_free(orc_tree* t) {
+  free(t->cfg); free(t->cost); free(t->parent); free(t->tgt); free(t->nsteps); free(t->nsafe);
+}
+
+/* outputs (caller-owned, capacity-checked): waypoints (cap_wp x 7), traj q/qd/qdd
+ * (cap_traj x 7), psg (cap_traj) */
+ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp, long cap_wp,
+                        double* tq, double* tqd, double* tqdd, double* psg, long cap_traj) {
+  memset(res, 0, sizeof(*res));
+  res->goal_node = -1;
+  res->first_fail = -1;
+  orc_ctx C;
+  memset(&C, 0, sizeof(C));
+  C.obs = cfg->obs; C.n_obs = cfg->n_obs; C.torque_mode = cfg->torque_mode; C.mass = cfg->mass;
+  C.cull = cfg->cull;
+  for (int k = 0; k < 7; ++k) { C.res[k] = 0.1; C.w[k] = 10.0; }
+  /* rrt_star.py:152-154 */
+  if (orc_collision(cfg->start, C.obs, C.n_obs, C.cull) || orc_collision(cfg->goal, C.obs, C.n_obs, C.cull)) {
+    res->status = 1;
+    return 1;
+  }
+  orc_tree T;
+  memset(&T, 0, sizeof(T));
+  tree_push(&T, cfg->start, 0.0, -1, 0, 0, 0);
+  long goal_n = -1;
+  long k = 0;
+  long rr = 0, ru = 0;
+  int B = cfg->batch > 0 ? cfg->batch : 1;
+  int replay = cfg->replay_random != 0 || cfg->replay_uniform != 0;
+  double* S = malloc(sizeof(double) * 7 * B);
+  int* dog = malloc(sizeof(int) * B);
+  int* nn = malloc(sizeof(int) * B);
+  int* ns = malloc(sizeof(int) * B);
+  int* nsafe = malloc(sizeof(int) * B);
+  double* last = malloc(sizeof(double) * 7 * B);
+  while (k < cfg->max_samples) {
+    int nb = (int)((cfg->max_samples - k) < B ? (cfg->max_samples - k) : B);
+    int goal_found = goal_n >= 0;
+    /* sample (rrt_star.py:160-161; utils.py:2941-2990) */
+    for (int j = 0; j < nb; ++j) {
+      long it = k + j;
+      if (replay) {
+        int dg;
+        if (goal_found) dg = 0;
+        else if (it == 0) dg = 1;
+        else {
+          if (rr >= cfg->n_replay_random) { res->status = 5; goto done; }
+          dg = cfg->replay_random[rr++] < cfg->goal_prob;
+        }
+        dog[j] = dg;
+        if (dg) memcpy(S + 7 * j, cfg->goal, sizeof(double) * 7);
+        else {
+          if (ru >= cfg->n_replay_uniform) { res->status = 5; goto done; }
+          const double* u = cfg->replay_uniform + 7 * ru++;
+          for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];
+        }
+      } else {
+        double u[8];
+        orc_philox_uniforms(cfg->seed, (uint64_t)it, u);
+        int dg = !goal_found && (it == 0 || u[7] < cfg->goal_prob);
+        dog[j] = dg;
+        if (dg) memcpy(S + 7 * j, cfg->goal, sizeof(double) * 7);
+        else for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];
+      }
+    }
+    long Tr = T.n;
+    /* nearest (rrt_star.py:9-14,171): argmin of distance, first index wins ties */
+    for (int j = 0; j < nb; ++j) {
+      double best = INFINITY;
+      int bi = 0;
+      for (long n = 0; n < Tr; ++n) {
+        double d = orc_dist(T.cfg + 7 * n, S + 7 * j, C.w);
+        if (d < best) { best = d; bi = (int)n; }
+      }
+      nn[j] = bi;
+    }
+    /* extend + safe path (rrt_star.py:172) */
+    for (int j = 0; j < nb; ++j)
+      nsafe[j] = orc_edge(&C, T.cfg + 7 * (long)nn[j], S + 7 * j, &ns[j], last + 7 * j);
+    /* insert in lane order + goal test + rewire against the round snapshot (:173-192) */
+    for (int j = 0; j < nb; ++j) {
+      if (nsafe[j] == 0) continue;
+      int par = nn[j];
+      double d = orc_dist(T.cfg + 7 * (long)par, last + 7 * j, C.w);
+      tree_push(&T, last + 7 * j, T.cost[par] + d, par, S + 7 * j, ns[j], nsafe[j]);
+      long nw = T.n - 1;
+      if (dog[j] && goal_n < 0 && orc_dist(T.cfg + 7 * nw, cfg->goal, C.w) < cfg->goal_tol) goal_n = nw;
+      for (long n = 0; n < Tr; ++n) {
+        double dn = orc_dist(T.cfg + 7 * n, T.cfg + 7 * nw, C.w);
+        if (!(dn < cfg->radius)) continue;
+        if (T.cost[n] + dn < T.cost[nw]) {
+          int rns;
+          double rl[7];
+          int rs = orc_edge(&C, T.cfg + 7 * n, T.cfg + 7 * nw, &rns, rl);
+          if (rs != 0 && orc_dist(T.cfg + 7 * nw, rl, C.w) < 1e-6) {
+            T.parent[nw] = (int)n;
+            T.cost[nw] = T.cost[n] + dn;
+            memcpy(T.tgt + 7 * nw, T.cfg + 7 * nw, 7 * sizeof(double));
+            T.nsteps[nw] = rns;
+            T.nsafe[nw] = rs;
+            res->n_rewires++;
+          }
+        }
+      }
+    }
+    k += nb;
+  }
+  res->n_samples = k;
+  res->n_nodes = T.n;
+  res->goal_node = goal_n;
+  res->edge_steps = C.edge_steps;
+  if (goal_n < 0) { res->status = 2; goto done; }
+  {
+    /* retrace (rrt_star.py:42-45,202): [start] + per edge (nsafe-1 regenerated points + cfg) */
+    long* chain = malloc(sizeof(long) * (size_t)T.n);
+    long L = 0;
+    for (long n = goal_n; n > 0; n = T.parent[n]) chain[L++] = n;
+    long W = 1;
+    for (long c = 0; c < L; ++c) W += T.nsafe[chain[c]];
+    res->n_waypoints = W;
+    if (W > cap_wp) { res->status = 6; free(chain); goto done; }
+    memcpy(wp, T.cfg, 7 * sizeof(double));
+    long o = 1;
+    for (long c = L - 1; c >= 0; --c) {
+      long n = chain[c];
+      double q[7];
+      memcpy(q, T.cfg + 7 * (long)T.parent[n], sizeof(q));
+      for (int i = 0; i < T.nsafe[n] - 1; ++i) {
+        orc_refine_step(q, T.tgt + 7 * n, T.nsteps[n], i);
+        memcpy(wp + 7 * o++, q, sizeof(q));
+      }
+      memcpy(wp + 7 * o++, T.cfg + 7 * n, 7 * sizeof(double));
+    }
+    free(chain);
+    if (!cfg->validate) goto done;
+    /* dynam_fn (panda_primitives.py:299-316) */
+    int ni = (int)(cfg->exec_time * 1000.0 / (double)W);
+    if (ni <= 0) { res->status = 4; goto done; }
+    long K = (W - 1) * (long)ni;
+    res->n_traj = K;
+    if (K > cap_traj) { res->status = 6; goto done; }
+    orc_minjerk(wp, (int)W, ni, tq, tqd, tqdd);
+    for (long i = 0; i < K; ++i) psg[i] = (cfg->exec_time * (double)i) / (double)K;
+    /* final validation (rrt_star.py:208-210) */
+    for (long i = 0; i < K; ++i) {
+      if (!orc_torque_ok(tq + 7 * i, tqd + 7 * i, tqdd + 7 * i, C.torque_mode, C.mass)) {
+        res->first_fail = i;
+        res->status = 3;
+        goto done;
+      }
+    }
+  }
+done:
+  tree_free(&T);
+  free(S); free(dog); free(nn); free(ns); free(nsafe); free(last);
+  return res->status;
+}
+
+ORC_API int orc_sizeof_cfg(void) { return (int)sizeof(orc_rrt_cfg); }
+ORC_API int orc_sizeof_result(void) { return (int)sizeof(orc_rrt_result); }
