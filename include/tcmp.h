@@ -1,0 +1,153 @@
+/*
+ * tcmp.h -- C-ABI of the MI355X torque-constrained RRT* engine (libtcmp.so).
+ *
+ * Plain pointers and sizes only: every array argument is a HOST pointer owned by the caller,
+ * row-major, fp64 configurations (7 per row), int32/int64 counts.  Every entry point returns
+ * an int status (0 = ok, < 0 = error; tcmp_last_error() gives a thread-local message).
+ * Calls are synchronous (the engine's stream is drained before return) unless noted.
+ *
+ * Each entry point names the reference interface it replaces
+ * (HIRO-group/torque_constrained_motion_planning @ v0, src/...).
+ */
+#ifndef TCMP_H_
+#define TCMP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tcmp_handle tcmp_handle;
+
+/* torque_test modes, panda_primitives.py:228-236 */
+#define TCMP_TORQUE_BASE 0 /* get_torque_limits_not_exceded_test_base   panda_primitives.py:13 */
+#define TCMP_TORQUE_NOV 1  /* get_torque_limits_not_exceded_test_v3_nov panda_primitives.py:118 */
+#define TCMP_TORQUE_RNE 2  /* get_torque_limits_not_exceded_test_v4     panda_primitives.py:155 */
+
+/* plan status codes (tcmp_plan_result.status) */
+#define TCMP_PLAN_OK 0            /* path found and validated (rrt_star.py:211) */
+#define TCMP_PLAN_START_GOAL_COLLISION 1 /* rrt_star.py:152-154 */
+#define TCMP_PLAN_NO_GOAL 2       /* rrt_star.py:199-201 */
+#define TCMP_PLAN_VALIDATION_FAILED 3 /* rrt_star.py:208-210 */
+#define TCMP_PLAN_MINJERK_ASSERT 4 /* min_jerk_v2.py:166 num_intervals == 0 */
+
+/* ---- lifetime -------------------------------------------------------------------------- */
+int tcmp_create(int device, tcmp_handle** out);
+int tcmp_destroy(tcmp_handle* h);
+const char* tcmp_last_error(void);
+int tcmp_device_count(int* n);
+int tcmp_version(void);
+
+/* Fixed obstacles (replaces Problem.fixed bodies + pybullet getClosestPoints,
+ * utils.py:3165-3218 / 2833-2849).  n_obs oriented boxes, 15 doubles each:
+ * centre(3), rotation R (9, row-major, columns = box axes, world frame), half extents(3). */
+int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs);
+
+/* ---- batched physics (host arrays in/out) ---------------------------------------------- */
+/* rne(q, qd, qdd) with add_payload(r, m) state made explicit: payload iff payload_mass > 0
+ * (rne.py:181-254).  q, qd, qdd, tau: n x 7. */
+int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                   int64_t n, double payload_mass, double* tau);
+
+/* torque test on n configurations (panda_primitives.py:13-193); qd/qdd may be NULL (zeros,
+ * the search-time call torque_fn(q)).  ok: n int32 (1 = within limits). */
+int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                   int64_t n, int32_t torque_mode, double payload_mass, int32_t* ok);
+
+/* collision_fn(q) on n configurations (utils.py:3165-3218): joint limits then every moving
+ * link hull vs every obstacle, penetration >= 0.04 m.  collides: n int32. */
+int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* collides);
+
+/* safe_path_force_aware(extend(from, to), collision, torque) for n edges (rrt_star.py:90-98,
+ * utils.py:3068-3077 with the given resolution vector (7, NULL = 0.1 as the planner uses)).
+ * n_safe = len(safe prefix), n_steps = len(extend), last = prefix[-1] (valid if n_safe>0). */
+int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64_t n,
+                     const double* resolutions, int32_t torque_mode, double payload_mass,
+                     int32_t* n_safe, int32_t* n_steps, double* last);
+
+/* argmin over tree nodes of the weighted distance (rrt_star.py:9-14,171), first index wins
+ * ties.  tree: T x 7, samples: n x 7, weights: 7 (NULL = 10 = 1/radius). */
+int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* samples,
+                 int64_t n, const double* weights, int32_t* idx);
+
+/* dynam_fn min-jerk sampling (panda_primitives.py:299-316 -> min_jerk_v2.py:80-222):
+ * n_wp waypoints (7 each), ni samples per segment; q/qd/qdd: (n_wp-1)*ni x 7. */
+int tcmp_minjerk(tcmp_handle* h, const double* waypoints, int64_t n_wp, int64_t ni, double* q,
+                 double* qd, double* qdd);
+
+/* final validation loop (rrt_star.py:208-210) + Conf.torques (utils.py:3376-3377, rne
+ * without payload).  first_fail = index of the first failing sample or -1.  tau may be NULL. */
+int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                       int64_t n, int32_t torque_mode, double payload_mass, int64_t* first_fail,
+                       double* tau);
+
+/* ---- the RRT* engine (rrt_star_force_aware, rrt_star.py:151-211) ------------------------ */
+typedef struct {
+  double start[7];
+  double goal[7];
+  double weights[7];      /* distance weights, 1/radius (panda_primitives.py:333-334) */
+  double resolutions[7];  /* extend resolutions (panda_primitives.py:337: radius) */
+  double radius;          /* rewire radius ([0.01], panda_primitives.py:346) */
+  double goal_probability;/* 0.2 (rrt_star.py:151) */
+  double goal_tolerance;  /* 1e-2 (rrt_star.py:178) */
+  double payload_mass;    /* Problem.payload_mass (torque tests) */
+  double execution_time;  /* Problem.execution_time (dynam_fn) */
+  uint64_t seed;          /* Philox4x32-10 key for device sampling */
+  int64_t max_nodes;      /* tree capacity (>= samples + 1) */
+  int32_t max_batch;      /* largest round size that will be used */
+  int32_t torque_mode;
+} tcmp_plan_cfg;
+
+typedef struct {
+  int32_t status;         /* TCMP_PLAN_* */
+  int32_t goal_found;
+  int64_t n_nodes;
+  int64_t n_samples;
+  int64_t goal_node;
+  int64_t n_waypoints;    /* len(goal_n.retrace()) */
+  int64_t n_traj;         /* min-jerk samples */
+  int64_t first_fail;
+  uint64_t edge_steps;    /* extend steps checked */
+  uint64_t pairs_tested;  /* link x obstacle pair classifications */
+  uint64_t pairs_sat;     /* pairs reaching the OBB SAT tier */
+  uint64_t pairs_exact;   /* exact hull tests */
+  uint64_t nn_pairs;      /* (candidate, node) distance evaluations */
+  double ms_nearest;      /* summed device time per kernel family (hipEvents) */
+  double ms_edges;
+  double ms_insert;
+  double ms_rewire;
+  double ms_finish;
+  int64_t launches_nearest;
+} tcmp_plan_result;
+
+/* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the
+ * tree and inserts the root.  result->status is set (0 or START_GOAL_COLLISION). */
+int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result);
+
+/* one round of nb candidates.  samples == NULL: device Philox sampling (batched frontier,
+ * at most one goal-biased lane per round).  Otherwise samples (nb x 7) and is_goal (nb) are
+ * the host's draws (nb = 1 reproduces the reference loop exactly).  goal_found (nullable)
+ * is written after a stream sync; pass NULL to keep rounds asynchronous. */
+int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
+                    int32_t* goal_found);
+
+/* device-sampled rounds of `batch` lanes until n_samples samples were drawn. */
+int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch);
+
+/* retrace + dynam_fn min-jerk + final torque validation (rrt_star.py:199-211); fills result. */
+int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* result);
+
+/* copy the finished plan: waypoints (n_waypoints x 7), trajectory q/qd/qdd (n_traj x 7),
+ * psg (n_traj), tau = Conf.torques without payload (n_traj x 7).  Any pointer may be NULL. */
+int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
+                    double* psg, double* tau);
+
+/* debug: tree snapshot (cfg n x 7, cost n, parent n). */
+int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32_t* parent,
+                   int64_t* n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -53,7 +53,7 @@ def lib():
         L.orc_minjerk.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp]
         L.orc_fk_links.argtypes = [_dp, _dp]
         L.orc_collision.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int]
-        L.orc_pair_pd.argtypes = [ctypes.c_int, _dp, _dp]
+        L.orc_pair_pd.argtypes = [ctypes.c_int, _dp, _dp, ctypes.c_int]
         L.orc_pair_pd.restype = ctypes.c_double
         L.orc_check_edge.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                      ctypes.c_int, _ip, _dp]
@@ -121,9 +121,11 @@ def collision(q, obs, cull=1):
     return bool(lib().orc_collision(_d(q), _d(o) if len(o) else None, len(o), int(cull)))
 
 
-def pair_pd(link, q, box):
+def pair_pd(link, q, box, method=0):
+    """method 0: brute-force exact hull PD; 1: Gauss-map exact hull PD; 2: outer OBB PD;
+    3: inner box PD."""
     q = _arr(q, (7,)); b = _arr(box, (15,))
-    return lib().orc_pair_pd(int(link), _d(q), _d(b))
+    return lib().orc_pair_pd(int(link), _d(q), _d(b), int(method))
 
 
 def check_edge(q1, q2, obs, torque_mode, mass, cull=1):

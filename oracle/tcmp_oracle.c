@@ -477,7 +477,7 @@ ORC_API double orc_hull_box_pd_local(int link, const double cl[3], const double 
   }
   /* hull edge x box axis */
   for (int e = e0; e < e1; ++e) {
-    const double* E = tcmp_geo_edges + 4 * e;
+    const double* E = tcmp_geo_edges + 16 * e;
     for (int i = 0; i < 3; ++i) {
       double ax[3] = {A[0 + i], A[3 + i], A[6 + i]};
       double n[3] = {E[1] * ax[2] - E[2] * ax[1], E[2] * ax[0] - E[0] * ax[2],
@@ -496,6 +496,63 @@ ORC_API double orc_hull_box_pd_local(int link, const double cl[3], const double 
       for (int j = 0; j < 3; ++j) rad += h[j] * fabs(n[0] * A[0 + j] + n[1] * A[3 + j] + n[2] * A[6 + j]);
       double ov = fmin(mx - (pc - rad), (pc + rad) - mn) / sqrt(len2);
       pd = fmin(pd, ov);
+    }
+  }
+  return pd;
+}
+
+/* Same penetration depth, computed over the facets of the Minkowski difference only
+ * (Gauss-map pruning): box faces (+/-a_i), hull facets (outward n_f), and hull edges whose
+ * adjacent facet normals straddle the plane normal to a box axis (silhouette edges).
+ * Mathematically identical to orc_hull_box_pd_local when the result is >= 0. */
+ORC_API double orc_hull_box_pd_gauss(int link, const double cl[3], const double A[9],
+                                     const double h[3]) {
+  const int v0 = tcmp_geo_vert_off[link], v1 = tcmp_geo_vert_off[link + 1];
+  const int f0 = tcmp_geo_plane_off[link], f1 = tcmp_geo_plane_off[link + 1];
+  const int e0 = tcmp_geo_edge_off[link], e1 = tcmp_geo_edge_off[link + 1];
+  double pd = INFINITY;
+  for (int i = 0; i < 3; ++i) {
+    double ax[3] = {A[0 + i], A[3 + i], A[6 + i]};
+    double mn = INFINITY, mx = -INFINITY;
+    for (int v = v0; v < v1; ++v) {
+      const double* P = tcmp_geo_verts + 4 * v;
+      double d = ax[0] * P[0] + ax[1] * P[1] + ax[2] * P[2];
+      mn = fmin(mn, d);
+      mx = fmax(mx, d);
+    }
+    double pc = ax[0] * cl[0] + ax[1] * cl[1] + ax[2] * cl[2];
+    pd = fmin(pd, mx - pc + h[i]);  /* facet +a_i */
+    pd = fmin(pd, pc + h[i] - mn);  /* facet -a_i */
+  }
+  for (int f = f0; f < f1; ++f) {
+    const double* P = tcmp_geo_planes + 8 * f;
+    double pc = P[0] * cl[0] + P[1] * cl[1] + P[2] * cl[2];
+    double rad = 0;
+    for (int i = 0; i < 3; ++i) rad += h[i] * fabs(P[0] * A[0 + i] + P[1] * A[3 + i] + P[2] * A[6 + i]);
+    pd = fmin(pd, P[3] - pc + rad);
+  }
+  for (int e = e0; e < e1; ++e) {
+    const double* E = tcmp_geo_edges + 16 * e;
+    const double* va = E + 4;
+    const double* n1 = E + 8;
+    const double* n2 = E + 12;
+    for (int i = 0; i < 3; ++i) {
+      double ax[3] = {A[0 + i], A[3 + i], A[6 + i]};
+      double s1 = n1[0] * ax[0] + n1[1] * ax[1] + n1[2] * ax[2];
+      double s2 = n2[0] * ax[0] + n2[1] * ax[1] + n2[2] * ax[2];
+      if (!(s1 * s2 < 0)) continue;
+      double m[3] = {E[1] * ax[2] - E[2] * ax[1], E[2] * ax[0] - E[0] * ax[2],
+                     E[0] * ax[1] - E[1] * ax[0]};
+      double len2 = m[0] * m[0] + m[1] * m[1] + m[2] * m[2];
+      if (len2 < 1e-24) continue;
+      if (m[0] * (n1[0] + n2[0]) + m[1] * (n1[1] + n2[1]) + m[2] * (n1[2] + n2[2]) < 0) {
+        m[0] = -m[0]; m[1] = -m[1]; m[2] = -m[2];
+      }
+      double hv = m[0] * va[0] + m[1] * va[1] + m[2] * va[2];
+      double pc = m[0] * cl[0] + m[1] * cl[1] + m[2] * cl[2];
+      double rad = 0;
+      for (int j = 0; j < 3; ++j) rad += h[j] * fabs(m[0] * A[0 + j] + m[1] * A[3 + j] + m[2] * A[6 + j]);
+      pd = fmin(pd, (hv - pc + rad) / sqrt(len2));
     }
   }
   return pd;
@@ -552,13 +609,23 @@ static int orc_pair_collides(int link, const double* fr, const double* ob, int c
     if ((ih[0] > 0) && obb_obb_pd(oc, oR, ih, cl, A, h) >= ORC_PEN) return 1;
   }
   if (n_exact) ++*n_exact;
+  if (cull == 2) return orc_hull_box_pd_gauss(link, cl, A, h) >= ORC_PEN;
   return orc_hull_box_pd_local(link, cl, A, h) >= ORC_PEN;
 }
 
-ORC_API double orc_pair_pd(int link, const double* q, const double* ob) {
+ORC_API double orc_pair_pd(int link, const double* q, const double* ob, int method) {
   double fr[120], cl[3], A[9];
   orc_fk_links(q, fr);
   box_to_link(fr + 12 * link, ob, cl, A);
+  if (method == 1) return orc_hull_box_pd_gauss(link, cl, A, ob + 12);
+  if (method == 2) {
+    const double* bx = tcmp_geo_boxes + 18 * link;
+    return obb_obb_pd(bx, bx + 3, bx + 12, cl, A, ob + 12);
+  }
+  if (method == 3) {
+    const double* bx = tcmp_geo_boxes + 18 * link;
+    return obb_obb_pd(bx, bx + 3, bx + 15, cl, A, ob + 12);
+  }
   return orc_hull_box_pd_local(link, cl, A, ob + 12);
 }
 
@@ -741,6 +808,7 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
   while (k < cfg->max_samples) {
     int nb = (int)((cfg->max_samples - k) < B ? (cfg->max_samples - k) : B);
     int goal_found = goal_n >= 0;
+    int goal_lane_taken = 0;
     /* sample (rrt_star.py:160-161; utils.py:2941-2990) */
     for (int j = 0; j < nb; ++j) {
       long it = k + j;
@@ -760,9 +828,13 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
           for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];
         }
       } else {
+        /* batched goal bias: a lane whose draw selects the goal becomes the round's goal
+         * sample only if no lower lane of the same round already is (B = 1: reference rule) */
         double u[8];
         orc_philox_uniforms(cfg->seed, (uint64_t)it, u);
         int dg = !goal_found && (it == 0 || u[7] < cfg->goal_prob);
+        if (dg && goal_lane_taken) dg = 0;
+        if (dg) goal_lane_taken = 1;
         dog[j] = dg;
         if (dg) memcpy(S + 7 * j, cfg->goal, sizeof(double) * 7);
         else for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];

@@ -1,0 +1,210 @@
+"""GPU parity: libtcmp (HIP, gfx950) against the CPU oracle and the reference's golden vectors.
+
+Tolerances: torques / trajectories within 1e-9 abs (north_star asks 1e-5 on joint angles
+and torques); integer results (nearest index, safe-prefix length, collision flags) exact.
+"""
+import glob
+import os
+import random
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+import oracle as O  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+TOL = 1e-9
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from torque_constrained_motion_planning_amd import _lib
+    e = _lib.engine(0)
+    return e
+
+
+def rand_q(rng, n):
+    return LO + (HI - LO) * rng.random((n, 7))
+
+
+def boxes(rng, n, aligned=True):
+    from torque_constrained_motion_planning_amd.scene import random_box_scene, obstacle_array
+    return obstacle_array(random_box_scene(rng, n, aligned=aligned))
+
+
+def test_rne_golden(eng):
+    z = np.load(os.path.join(GOLDEN, "rne_golden.npz"))
+    for m in (0, 2, 5):
+        t = "m%d" % m
+        q, qd, qdd = z["q_" + t], z["qd_" + t], z["qdd_" + t]
+        ts = eng.rne(q, np.zeros_like(q), np.zeros_like(q), float(m))
+        td = eng.rne(q, qd, qdd, float(m))
+        assert np.abs(ts - z["tau_static_" + t]).max() < TOL
+        assert np.abs(td - z["tau_dyn_" + t]).max() < TOL
+
+
+def test_torque_tests_vs_oracle(eng):
+    rng = np.random.default_rng(11)
+    q = rand_q(rng, 3000)
+    qd = rng.uniform(-2, 2, q.shape)
+    qdd = rng.uniform(-6, 6, q.shape)
+    for mode in (0, 1, 2):
+        for mass in (0.0, 0.005, 2.0, 5.0, 9.0):
+            ok_s = eng.torque_ok(q, mode, mass)
+            ok_d = eng.torque_ok(q, mode, mass, qd=qd, qdd=qdd)
+            ref_s = np.array([O.torque_ok(x, mode, mass) for x in q])
+            ref_d = np.array([O.torque_ok(x, mode, mass, a, b) for x, a, b in zip(q, qd, qdd)])
+            assert (ok_s == ref_s).all(), (mode, mass)
+            assert (ok_d == ref_d).all(), (mode, mass)
+
+
+def test_minjerk_golden(eng):
+    z = np.load(os.path.join(GOLDEN, "minjerk_golden.npz"))
+    for c in range(int(z["ncases"])):
+        P, ni = z["P%d" % c], int(z["ni%d" % c])
+        q, qd, qdd = eng.minjerk(P, ni)
+        assert np.abs(q - z["x%d" % c]).max() < 1e-12
+        assert np.abs(qd - z["v%d" % c]).max() < 1e-12
+        assert np.abs(qdd - z["a%d" % c]).max() < 1e-12
+
+
+def test_collision_vs_oracle(eng):
+    rng = np.random.default_rng(5)
+    for n_obs, aligned in ((0, True), (4, True), (16, True), (16, False), (64, True)):
+        obs = boxes(rng, n_obs, aligned) if n_obs else np.zeros((0, 15))
+        eng.set_scene(obs)
+        q = rand_q(rng, 2000)
+        q[:50] = LO - 1e-3 + (HI - LO + 2e-3) * rng.random((50, 7))  # some out of limits
+        got = eng.collides(q)
+        # oracle: bounds + Gauss-map exact test; brute-force exact test on a subset
+        ref = np.array([O.collision(x, obs, cull=2) for x in q])
+        assert (got == ref).all(), (n_obs, aligned, np.nonzero(got != ref))
+        sub = q[:60]
+        ref0 = np.array([O.collision(x, obs[:8], cull=0) for x in sub])
+        eng.set_scene(obs[:8])
+        assert (eng.collides(sub) == ref0).all()
+
+
+def test_check_edges_vs_oracle(eng):
+    rng = np.random.default_rng(7)
+    for n_obs, mode, mass in ((0, 2, 5.0), (4, 1, 2.0), (16, 2, 5.0), (16, 0, 0.0)):
+        obs = boxes(rng, n_obs) if n_obs else np.zeros((0, 15))
+        eng.set_scene(obs)
+        a = rand_q(rng, 400)
+        b = rand_q(rng, 400)
+        b[:200] = np.clip(a[:200] + rng.normal(0, 0.3, (200, 7)), LO, HI)
+        ns, nt, last = eng.check_edges(a, b, mode, mass)
+        for i in range(len(a)):
+            s, n, l = O.check_edge(a[i], b[i], obs, mode, mass, cull=2)
+            assert ns[i] == s and nt[i] == n, (i, ns[i], s, nt[i], n)
+            if s:
+                assert np.array_equal(last[i], l), i
+
+
+def test_nearest_exact(eng):
+    rng = np.random.default_rng(3)
+    tree = rand_q(rng, 5000)
+    tree[100] = tree[7]  # duplicate: first index must win
+    s = rand_q(rng, 1000)
+    s[0] = tree[7]
+    idx = eng.nearest(tree, s)
+    d = ((s[:, None, :] - tree[None, :, :]) ** 2).sum(-1)
+    assert (idx == d.argmin(1)).all()
+    assert idx[0] == 7
+
+
+def test_validate_traj_vs_oracle(eng):
+    rng = np.random.default_rng(9)
+    wp = rand_q(rng, 6)
+    for ni in (40, 200):
+        q, qd, qdd = eng.minjerk(wp, ni)
+        for mode, mass in ((1, 5.0), (2, 5.0), (2, 0.0), (0, 0.0)):
+            ff, tau = eng.validate(q, qd, qdd, mode, mass)
+            ref_ff = -1
+            for i in range(len(q)):
+                if not O.torque_ok(q[i], mode, mass, qd[i], qdd[i]):
+                    ref_ff = i
+                    break
+            assert ff == ref_ff
+            assert np.abs(tau - O.rne(q, qd, qdd, 0.0)).max() < TOL
+
+
+RRT_GOLDEN = sorted(glob.glob(os.path.join(GOLDEN, "rrt_*.npz")))
+
+
+@pytest.mark.parametrize("path", RRT_GOLDEN, ids=[os.path.basename(p) for p in RRT_GOLDEN])
+def test_rrt_golden_drop_in(eng, path):
+    """The package's rrt_star_force_aware with its own closures, seeded like the reference
+    run, reproduces the reference RRT* output (waypoints, q, qd, qdd, psg)."""
+    from torque_constrained_motion_planning_amd import panda_primitives as PP
+    from torque_constrained_motion_planning_amd import utils as U
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_force_aware
+    z = np.load(path)
+    mode = int(z["mode"])
+    mass = float(z["mass"])
+    prob = U.Problem(U.PandaRobot(), list(z["obs"]), U.Payload(mass), mass, float(z["exec_time"]),
+                     torque_test={0: "base", 1: "nov", 2: "rne"}[mode])
+    torque_fn = PP.select_torque_test(prob)
+    resolutions = 0.2 ** np.ones(7)
+    radius = resolutions / 2
+    dyn = PP.get_dynamics_fn_v5(prob, resolutions)
+    joints = U.get_arm_joints(prob.robot)
+    sample = U.get_sample_fn(prob.robot, joints)
+    dist = U.get_distance_fn(prob.robot, joints, weights=np.reciprocal(radius))
+    ext = U.get_extend_fn(prob.robot, joints, resolutions=radius)
+    coll = U.get_collision_fn(prob.robot, joints, list(z["obs"]), self_collisions=False)
+    seed = int(z["seed"])
+    random.seed(seed)
+    np.random.seed(seed)
+    path_, vels, accels, psg = rrt_star_force_aware(
+        tuple(z["start"]), tuple(z["goal"]), dist, sample, ext, coll, torque_fn, dyn,
+        radius=[0.01], max_time=50, max_iterations=int(z["iters"]))
+    assert (path_ is not None) == bool(z["found"])
+    if path_ is None:
+        return
+    q = np.array(path_)
+    assert len(q) == int(z["n_traj"])
+    idx = z["traj_idx"]
+    assert np.abs(q[idx] - z["q"]).max() < 1e-9
+    assert np.abs(np.array(vels)[idx] - z["qd"]).max() < 1e-9
+    assert np.abs(np.array(accels)[idx] - z["qdd"]).max() < 1e-9
+    assert np.abs(np.array(psg)[idx] - z["psg"]).max() < 1e-12
+    assert np.abs(q.sum(0) - z["sum_q"]).max() < 1e-6
+
+
+@pytest.mark.parametrize("batch,n_obs,mode,mass", [(1, 4, 2, 5.0), (64, 8, 1, 2.0),
+                                                   (256, 16, 2, 5.0), (4096, 16, 2, 5.0)])
+def test_batched_frontier_vs_oracle(eng, batch, n_obs, mode, mass):
+    """Device-sampled batched rounds (Philox) == the oracle's batched restatement."""
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    rng = np.random.default_rng(100 + batch)
+    start = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])
+    while True:
+        goal = rand_q(rng, 1)[0]
+        obs = boxes(rng, n_obs)
+        if not (O.collision(start, obs) or O.collision(goal, obs)) and O.torque_ok(goal, mode, mass):
+            break
+    n_samples = 3 * batch + 17 if batch > 1 else 60
+    (path, vels, accels, psg), r, raw = rrt_star_batched(
+        start, goal, obs, mode, mass, 1.0, n_samples, batch=batch, seed=1234 + batch, engine=eng)
+    ref = O.rrt_run(start, goal, n_samples, obs, mode, mass, 1.0, batch=batch, seed=1234 + batch,
+                    cull=2)
+    assert r.n_nodes == ref["n_nodes"]
+    assert r.edge_steps == ref["edge_steps"]
+    assert r.goal_node == ref["goal_node"]
+    cfg, cost, par, n = eng.plan_tree(r.n_nodes)
+    assert n == ref["n_nodes"]
+    if ref["status"] in (0, 3):
+        assert r.status == ref["status"]
+        assert r.n_waypoints == ref["n_waypoints"]
+        assert np.abs(raw["waypoints"] - ref["waypoints"]).max() < 1e-12
+        assert np.abs(raw["q"] - ref["q"]).max() < 1e-9
+        assert np.abs(raw["qd"] - ref["qd"]).max() < 1e-9
+        assert np.abs(raw["qdd"] - ref["qdd"]).max() < 1e-9
+    else:
+        assert r.status == ref["status"]

@@ -126,20 +126,26 @@ def link_data(stl, flip_z_pi):
     # merge duplicate planes (coplanar triangles)
     _, idx = np.unique(np.round(planes[:, :4], 10), axis=0, return_index=True)
     planes = planes[np.sort(idx)]
-    edges = set()
-    for s in h.simplices:
+    # hull edges with their two adjacent facets (Gauss-map arcs): edge record =
+    # direction e (unit), endpoint va, adjacent facet normals n1, n2
+    tri_plane = []
+    for eq in h.equations:
+        nrm = eq[:3] / np.linalg.norm(eq[:3])
+        key = np.round(np.concatenate([nrm, [(v @ nrm).max()]]), 10)
+        tri_plane.append(int(np.where(np.all(np.round(planes[:, :4], 10) == key, axis=1))[0][0]))
+    adj = {}
+    for ti, s in enumerate(h.simplices):
         for a, b in ((0, 1), (1, 2), (0, 2)):
-            edges.add(tuple(sorted((int(s[a]), int(s[b])))))
+            adj.setdefault(tuple(sorted((int(s[a]), int(s[b])))), []).append(tri_plane[ti])
     dirs = []
-    for a, b in sorted(edges):
+    for (a, b), fs in sorted(adj.items()):
+        assert len(fs) == 2, "non-manifold hull edge"
+        if fs[0] == fs[1]:
+            continue  # edge interior to a merged facet
         e = v[b] - v[a]
         e = e / np.linalg.norm(e)
-        if e[np.argmax(np.abs(e))] < 0:
-            e = -e
-        dirs.append(e)
+        dirs.append(np.concatenate([e, v[a], planes[fs[0], :3], planes[fs[1], :3]]))
     dirs = np.array(dirs)
-    _, idx = np.unique(np.round(dirs, 10), axis=0, return_index=True)
-    dirs = dirs[np.sort(idx)]
     c, R, half = obb_fit(v)
     ih = inner_box(c, R, half, planes[:, [0, 1, 2, 3]])
     return dict(verts=v, planes=planes, edges=dirs, obb_c=c, obb_R=R, obb_half=half,
@@ -171,34 +177,38 @@ def main():
     L.append(" * Panda collision geometry (link frames), from reference")
     L.append(" * src/models/panda_mod.urdf + src/models/meshes/panda/collision/ (STL).")
     L.append(" * Data only: included by the HIP engine and by the CPU oracle. */")
+    L.append("#ifndef TCMP_GEO_QUAL")
+    L.append("#define TCMP_GEO_QUAL static const")
+    L.append("#endif")
     L.append("#define TCMP_NLINKS 10")
     L.append("#define TCMP_TOTAL_VERTS %d" % ov[-1])
     L.append("#define TCMP_TOTAL_PLANES %d" % of[-1])
     L.append("#define TCMP_TOTAL_EDGES %d" % oe[-1])
-    L.append("static const int tcmp_geo_vert_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, ov)))
-    L.append("static const int tcmp_geo_plane_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, of)))
-    L.append("static const int tcmp_geo_edge_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, oe)))
+    L.append("TCMP_GEO_QUAL int tcmp_geo_vert_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, ov)))
+    L.append("TCMP_GEO_QUAL int tcmp_geo_plane_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, of)))
+    L.append("TCMP_GEO_QUAL int tcmp_geo_edge_off[TCMP_NLINKS + 1] = {%s};" % ", ".join(map(str, oe)))
     L.append("/* verts: x y z 0 (padded to 4 doubles) */")
-    L.append("static const double tcmp_geo_verts[TCMP_TOTAL_VERTS * 4] = {")
+    L.append("TCMP_GEO_QUAL double tcmp_geo_verts[TCMP_TOTAL_VERTS * 4] = {")
     for d in links:
         for p in d["verts"]:
             L.append("  %s, %s, %s, 0.0," % tuple(fmt(x) for x in p))
     L.append("};")
     L.append("/* planes: nx ny nz dmax wmin 0 0 0 (padded to 8 doubles) */")
-    L.append("static const double tcmp_geo_planes[TCMP_TOTAL_PLANES * 8] = {")
+    L.append("TCMP_GEO_QUAL double tcmp_geo_planes[TCMP_TOTAL_PLANES * 8] = {")
     for d in links:
         for p in d["planes"]:
             L.append("  %s, %s, %s, %s, %s, 0.0, 0.0, 0.0," % tuple(fmt(x) for x in p))
     L.append("};")
-    L.append("/* edge directions: ex ey ez 0 */")
-    L.append("static const double tcmp_geo_edges[TCMP_TOTAL_EDGES * 4] = {")
+    L.append("/* hull edges: e(3) 0 | endpoint va(3) 0 | facet normal n1(3) 0 | n2(3) 0 */")
+    L.append("TCMP_GEO_QUAL double tcmp_geo_edges[TCMP_TOTAL_EDGES * 16] = {")
     for d in links:
         for p in d["edges"]:
-            L.append("  %s, %s, %s, 0.0," % tuple(fmt(x) for x in p))
+            vals = list(p[0:3]) + [0.0] + list(p[3:6]) + [0.0] + list(p[6:9]) + [0.0] + list(p[9:12]) + [0.0]
+            L.append("  " + ", ".join(fmt(x) for x in vals) + ",")
     L.append("};")
     L.append("/* per link box data: obb centre(3) axes R row-major (9, columns = box axes) "
              "outer half(3) inner half(3) -> 18 doubles */")
-    L.append("static const double tcmp_geo_boxes[TCMP_NLINKS * 18] = {")
+    L.append("TCMP_GEO_QUAL double tcmp_geo_boxes[TCMP_NLINKS * 18] = {")
     for d in links:
         vals = list(d["obb_c"]) + list(d["obb_R"].reshape(-1)) + list(d["obb_half"]) + list(d["in_half"])
         L.append("  " + ", ".join(fmt(x) for x in vals) + ",")

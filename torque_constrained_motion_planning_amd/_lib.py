@@ -1,0 +1,281 @@
+"""ctypes binding of libtcmp.so (include/tcmp.h).
+
+The product path has no fallback: if the HIP library is missing or no GPU is visible, every
+entry point raises.  Nothing here imports torch or the CPU oracle.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libtcmp.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_i32p = ctypes.POINTER(ctypes.c_int32)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+TORQUE_BASE, TORQUE_NOV, TORQUE_RNE = 0, 1, 2
+PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_MINJERK_ASSERT = range(5)
+
+# C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)
+EXPORTS = [
+    "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
+    "tcmp_set_scene", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
+    "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
+    "tcmp_plan_fetch", "tcmp_plan_tree",
+]
+
+
+class PlanCfg(ctypes.Structure):
+    _fields_ = [
+        ("start", ctypes.c_double * 7), ("goal", ctypes.c_double * 7),
+        ("weights", ctypes.c_double * 7), ("resolutions", ctypes.c_double * 7),
+        ("radius", ctypes.c_double), ("goal_probability", ctypes.c_double),
+        ("goal_tolerance", ctypes.c_double), ("payload_mass", ctypes.c_double),
+        ("execution_time", ctypes.c_double), ("seed", ctypes.c_uint64),
+        ("max_nodes", ctypes.c_int64), ("max_batch", ctypes.c_int32),
+        ("torque_mode", ctypes.c_int32),
+    ]
+
+
+class PlanResult(ctypes.Structure):
+    _fields_ = [
+        ("status", ctypes.c_int32), ("goal_found", ctypes.c_int32),
+        ("n_nodes", ctypes.c_int64), ("n_samples", ctypes.c_int64),
+        ("goal_node", ctypes.c_int64), ("n_waypoints", ctypes.c_int64),
+        ("n_traj", ctypes.c_int64), ("first_fail", ctypes.c_int64),
+        ("edge_steps", ctypes.c_uint64), ("pairs_tested", ctypes.c_uint64),
+        ("pairs_sat", ctypes.c_uint64), ("pairs_exact", ctypes.c_uint64),
+        ("nn_pairs", ctypes.c_uint64),
+        ("ms_nearest", ctypes.c_double), ("ms_edges", ctypes.c_double),
+        ("ms_insert", ctypes.c_double), ("ms_rewire", ctypes.c_double),
+        ("ms_finish", ctypes.c_double), ("launches_nearest", ctypes.c_int64),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class TcmpError(RuntimeError):
+    pass
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load_library(path=LIB_PATH):
+    """Load libtcmp.so (no compute call: usable on a CPU-only host)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise TcmpError("libtcmp.so not built (%s): run __graft_entry__.build()" % path)
+        L = ctypes.CDLL(path)
+        vp = ctypes.c_void_p
+        L.tcmp_last_error.restype = ctypes.c_char_p
+        L.tcmp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
+        L.tcmp_destroy.argtypes = [vp]
+        L.tcmp_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.tcmp_set_scene.argtypes = [vp, _dp, ctypes.c_int32]
+        L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
+        L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
+                                     ctypes.c_double, _i32p]
+        L.tcmp_check_configs.argtypes = [vp, _dp, ctypes.c_int64, _i32p]
+        L.tcmp_check_edges.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, ctypes.c_int32,
+                                       ctypes.c_double, _i32p, _i32p, _dp]
+        L.tcmp_nearest.argtypes = [vp, _dp, ctypes.c_int64, _dp, ctypes.c_int64, _dp, _i32p]
+        L.tcmp_minjerk.argtypes = [vp, _dp, ctypes.c_int64, ctypes.c_int64, _dp, _dp, _dp]
+        L.tcmp_validate_traj.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
+                                         ctypes.c_double, _i64p, _dp]
+        L.tcmp_plan_begin.argtypes = [vp, ctypes.POINTER(PlanCfg), ctypes.POINTER(PlanResult)]
+        L.tcmp_plan_round.argtypes = [vp, _dp, _u8p, ctypes.c_int32, _i32p]
+        L.tcmp_plan_run.argtypes = [vp, ctypes.c_int64, ctypes.c_int32]
+        L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
+        L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
+        L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
+        _lib = L
+        return L
+
+
+def _d(a):
+    return None if a is None else a.ctypes.data_as(_dp)
+
+
+def _rows(x, name="array"):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64))
+    if a.ndim == 1:
+        a = a.reshape(1, -1)
+    if a.shape[-1] != 7:
+        raise ValueError("%s must have 7 columns, got shape %s" % (name, a.shape))
+    return a.reshape(-1, 7)
+
+
+class Engine:
+    """One HIP device handle (tcmp_handle).  Not thread-safe; one per (thread, device)."""
+
+    def __init__(self, device=0):
+        self.L = load_library()
+        h = ctypes.c_void_p()
+        self._check(self.L.tcmp_create(int(device), ctypes.byref(h)))
+        self.h = h
+        self.device = device
+        self._scene_key = None
+
+    def _check(self, rc):
+        if rc != 0:
+            raise TcmpError("tcmp error %d: %s" % (rc, self.L.tcmp_last_error().decode()))
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tcmp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- scene ------------------------------------------------------------------------
+    def set_scene(self, obb):
+        obb = np.ascontiguousarray(np.asarray(obb, dtype=np.float64).reshape(-1, 15))
+        key = obb.tobytes()
+        if key == self._scene_key:
+            return
+        self._check(self.L.tcmp_set_scene(self.h, _d(obb) if len(obb) else None, len(obb)))
+        self._scene_key = key
+
+    # ---- batched physics --------------------------------------------------------------
+    def rne(self, q, qd, qdd, payload_mass=0.0):
+        q = _rows(q, "q"); qd = _rows(qd, "qd"); qdd = _rows(qdd, "qdd")
+        tau = np.zeros_like(q)
+        self._check(self.L.tcmp_rne_batch(self.h, _d(q), _d(qd), _d(qdd), len(q),
+                                          float(payload_mass), _d(tau)))
+        return tau
+
+    def torque_ok(self, q, mode, mass, qd=None, qdd=None):
+        q = _rows(q, "q")
+        qd = None if qd is None else _rows(qd, "qd")
+        qdd = None if qdd is None else _rows(qdd, "qdd")
+        ok = np.zeros(len(q), dtype=np.int32)
+        self._check(self.L.tcmp_torque_ok(self.h, _d(q), _d(qd), _d(qdd), len(q), int(mode),
+                                          float(mass), ok.ctypes.data_as(_i32p)))
+        return ok.astype(bool)
+
+    def collides(self, q):
+        q = _rows(q, "q")
+        out = np.zeros(len(q), dtype=np.int32)
+        self._check(self.L.tcmp_check_configs(self.h, _d(q), len(q), out.ctypes.data_as(_i32p)))
+        return out.astype(bool)
+
+    def check_edges(self, q_from, q_to, mode, mass, resolutions=None):
+        a = _rows(q_from, "from"); b = _rows(q_to, "to")
+        n = len(a)
+        ns = np.zeros(n, dtype=np.int32); nt = np.zeros(n, dtype=np.int32)
+        last = np.zeros((n, 7))
+        res = None if resolutions is None else np.ascontiguousarray(resolutions, dtype=np.float64)
+        self._check(self.L.tcmp_check_edges(self.h, _d(a), _d(b), n, _d(res), int(mode),
+                                            float(mass), ns.ctypes.data_as(_i32p),
+                                            nt.ctypes.data_as(_i32p), _d(last)))
+        return ns, nt, last
+
+    def nearest(self, tree, samples, weights=None):
+        t = _rows(tree, "tree"); s = _rows(samples, "samples")
+        idx = np.zeros(len(s), dtype=np.int32)
+        w = None if weights is None else np.ascontiguousarray(weights, dtype=np.float64)
+        self._check(self.L.tcmp_nearest(self.h, _d(t), len(t), _d(s), len(s), _d(w),
+                                        idx.ctypes.data_as(_i32p)))
+        return idx
+
+    def minjerk(self, waypoints, ni):
+        P = _rows(waypoints, "waypoints")
+        if int(ni) <= 0:
+            raise AssertionError("Invalid number of intervals chosen (must be greater than 0)")
+        K = (len(P) - 1) * int(ni)
+        q = np.zeros((K, 7)); qd = np.zeros((K, 7)); qdd = np.zeros((K, 7))
+        if K:
+            self._check(self.L.tcmp_minjerk(self.h, _d(P), len(P), int(ni), _d(q), _d(qd), _d(qdd)))
+        return q, qd, qdd
+
+    def validate(self, q, qd, qdd, mode, mass, want_tau=True):
+        q = _rows(q); qd = _rows(qd); qdd = _rows(qdd)
+        ff = ctypes.c_int64(-1)
+        tau = np.zeros_like(q) if want_tau else None
+        self._check(self.L.tcmp_validate_traj(self.h, _d(q), _d(qd), _d(qdd), len(q), int(mode),
+                                              float(mass), ctypes.byref(ff), _d(tau)))
+        return ff.value, tau
+
+    # ---- planner ----------------------------------------------------------------------
+    def plan_begin(self, start, goal, mode, mass, exec_time, max_nodes, max_batch, seed=0,
+                   weights=None, resolutions=None, radius=0.01, goal_probability=0.2,
+                   goal_tolerance=1e-2):
+        cfg = PlanCfg()
+        cfg.start[:] = [float(x) for x in start]
+        cfg.goal[:] = [float(x) for x in goal]
+        cfg.weights[:] = [float(x) for x in (weights if weights is not None else [10.0] * 7)]
+        cfg.resolutions[:] = [float(x) for x in (resolutions if resolutions is not None else [0.1] * 7)]
+        cfg.radius = float(radius)
+        cfg.goal_probability = float(goal_probability)
+        cfg.goal_tolerance = float(goal_tolerance)
+        cfg.payload_mass = float(mass)
+        cfg.execution_time = float(exec_time)
+        cfg.seed = int(seed)
+        cfg.max_nodes = int(max_nodes)
+        cfg.max_batch = int(max_batch)
+        cfg.torque_mode = int(mode)
+        res = PlanResult()
+        self._check(self.L.tcmp_plan_begin(self.h, ctypes.byref(cfg), ctypes.byref(res)))
+        return res.status
+
+    def plan_round(self, samples=None, is_goal=None, nb=None, sync=True):
+        gf = ctypes.c_int32(0)
+        if samples is not None:
+            s = _rows(samples)
+            g = np.ascontiguousarray(np.asarray(is_goal, dtype=np.uint8).reshape(-1))
+            self._check(self.L.tcmp_plan_round(self.h, _d(s), g.ctypes.data_as(_u8p), len(s),
+                                               ctypes.byref(gf) if sync else None))
+        else:
+            self._check(self.L.tcmp_plan_round(self.h, None, None, int(nb),
+                                               ctypes.byref(gf) if sync else None))
+        return bool(gf.value)
+
+    def plan_run(self, n_samples, batch):
+        self._check(self.L.tcmp_plan_run(self.h, int(n_samples), int(batch)))
+
+    def plan_finish(self):
+        r = PlanResult()
+        self._check(self.L.tcmp_plan_finish(self.h, ctypes.byref(r)))
+        return r
+
+    def plan_fetch(self, r):
+        W, K = r.n_waypoints, r.n_traj
+        wp = np.zeros((W, 7)); q = np.zeros((K, 7)); qd = np.zeros((K, 7))
+        qdd = np.zeros((K, 7)); psg = np.zeros(K); tau = np.zeros((K, 7))
+        self._check(self.L.tcmp_plan_fetch(self.h, _d(wp), _d(q), _d(qd), _d(qdd), _d(psg), _d(tau)))
+        return dict(waypoints=wp, q=q, qd=qd, qdd=qdd, psg=psg, tau=tau)
+
+    def plan_tree(self, cap):
+        cfg = np.zeros((cap, 7)); cost = np.zeros(cap); par = np.zeros(cap, dtype=np.int32)
+        n = ctypes.c_int64(0)
+        self._check(self.L.tcmp_plan_tree(self.h, int(cap), _d(cfg), _d(cost),
+                                          par.ctypes.data_as(_i32p), ctypes.byref(n)))
+        m = min(cap, n.value)
+        return cfg[:m], cost[:m], par[:m], n.value
+
+
+_engines = {}
+
+
+def engine(device=0):
+    """Process-wide engine per device (the Python API's default handle)."""
+    e = _engines.get(device)
+    if e is None:
+        e = Engine(device)
+        _engines[device] = e
+    return e

@@ -1,0 +1,635 @@
+// tcmp_device.h -- per-lane device math of the torque-constrained RRT* hot path (gfx950).
+//
+// Everything here is fp64 (the reference is numpy float64).  One wavefront lane owns one
+// configuration / edge; the only cross-lane code is the wave-cooperative exact
+// hull-vs-box test (exact_pd_wave), which every lane of the wave must reach together.
+//
+// Reference semantics restated (file:line in /root/reference/src):
+//   extend/refine      utils.py:3031-3041, 3068-3077
+//   distance           utils.py:3010-3017
+//   limits             utils.py:3154-3163, 1150-1154
+//   collision          utils.py:3165-3218, 2833-2880 (pybullet hull closest points, -0.04)
+//   rne                rne.py:198-254 (spatial RNE, modified DH rne.py:46-63)
+//   torque tests       panda_primitives.py:13-16, 118-153, 155-193
+//   min-jerk           min_jerk_v2.py:80-222, panda_primitives.py:295-318
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define TCMP_GEO_QUAL static constexpr
+#include "panda_geometry.inc"
+
+namespace tcmp {
+
+constexpr double kPen = 0.04;  // utils.py:2781 MAX_DISTANCE, used as distance=-0.04
+
+// panda_mod.urdf joint limits / efforts
+constexpr double kLo[7] = {-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973};
+constexpr double kHi[7] = {2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973};
+constexpr double kEffort[7] = {87.0, 87.0, 87.0, 87.0, 12.0, 12.0, 12.0};
+
+// modified DH (rne.py:47-54): a, d, cos(alpha), sin(alpha) with libm values of +-pi/2
+constexpr double kC90 = 6.123233995736766e-17;
+constexpr double kDhA[8] = {0.0, 0.0, 0.0, 0.0825, -0.0825, 0.0, 0.088, 0.0};
+constexpr double kDhD[8] = {0.333, 0.0, 0.316, 0.0, 0.384, 0.0, 0.0, 0.107};
+constexpr double kDhCa[8] = {1.0, kC90, kC90, kC90, kC90, kC90, kC90, 1.0};
+constexpr double kDhSa[8] = {0.0, -1.0, 1.0, 1.0, -1.0, 1.0, 1.0, 0.0};
+
+// inertials rne.py:65-136 (link1..7); composite flange+hand(+payload) handled in rne()
+constexpr double kMass[7] = {4.970684, 0.646926, 3.228604, 3.587895, 1.225946, 1.666555,
+                             7.35522e-01};
+constexpr double kCom[7][3] = {{3.875e-03, 2.081e-03, -0.1750},
+                               {-3.141e-03, -2.872e-02, 3.495e-03},
+                               {2.7518e-02, 3.9252e-02, -6.6502e-02},
+                               {-5.317e-02, 1.04419e-01, 2.7454e-02},
+                               {-1.1953e-02, 4.1065e-02, -3.8437e-02},
+                               {6.0149e-02, -1.4117e-02, -1.0517e-02},
+                               {1.0517e-02, -4.252e-03, 6.1597e-02}};
+// ixx ixy ixz iyy iyz izz
+constexpr double kInertia[7][6] = {
+    {7.0337e-01, -1.3900e-04, 6.7720e-03, 7.0661e-01, 1.9169e-02, 9.1170e-03},
+    {7.9620e-03, -3.9250e-03, 1.0254e-02, 2.8110e-02, 7.0400e-04, 2.5995e-02},
+    {3.7242e-02, -4.7610e-03, -1.1396e-02, 3.6155e-02, -1.2805e-02, 1.0830e-02},
+    {2.5853e-02, 7.7960e-03, -1.3320e-03, 1.9552e-02, 8.6410e-03, 2.8323e-02},
+    {3.5549e-02, -2.1170e-03, -4.0370e-03, 2.9474e-02, 2.2900e-04, 8.6270e-03},
+    {1.9640e-03, 1.0900e-04, -1.1580e-03, 4.3540e-03, 3.4100e-04, 5.4330e-03},
+    {1.2516e-02, -4.2800e-04, -1.1960e-03, 1.0027e-02, -7.4100e-04, 4.8150e-03}};
+constexpr double kHandMass = 0.68;         // rne.py:134
+constexpr double kFlangeHandI = 0.101;     // link8 I=0.001 (rne.py:73) + hand I=0.1 (:74)
+constexpr double kPayloadR = 0.165;        // new_inertia([0,0,0.14+0.025], m) (rne.py:187)
+constexpr double kPayloadMin = 0.01;       // panda_primitives.py:142,178
+
+// URDF joint origins (panda_mod.urdf joint1..7) -- pybullet link frames for collision
+constexpr double kJx[7] = {0, 0, 0, 0.0825, -0.0825, 0, 0.088};
+constexpr double kJy[7] = {0, 0, -0.316, 0, 0.384, 0, 0};
+constexpr double kJz[7] = {0.333, 0, 0, 0, 0, 0, 0};
+constexpr double kCr = 4.8965888601467475e-12;  // cos(1.57079632679)
+constexpr double kJcr[7] = {1.0, kCr, kCr, kCr, kCr, kCr, kCr};
+constexpr double kJsr[7] = {0.0, -1.0, 1.0, 1.0, -1.0, 1.0, 1.0};
+constexpr double kFlangeZ = 0.107;
+constexpr double kHandCy = 0.7071067811868645, kHandSy = -0.7071067811862305;  // rz(-0.785398163397)
+constexpr double kFingerZ = 0.0584, kFingerOpen = 0.04;
+
+// ------------------------------------------------------------------------------------------
+// scene / geometry views
+// ------------------------------------------------------------------------------------------
+struct Geo {
+  const double* __restrict__ verts;   // [V][4]
+  const double* __restrict__ planes;  // [F][8] n(3) dmax wmin
+  const double* __restrict__ edges;   // [E][16] e | va | n1 | n2
+};
+
+// obstacle record on device: c(3) B(9 row-major, columns = axes) h(3) aligned(1) pad -> 16
+struct Scene {
+  const double* __restrict__ obs;  // [n][16]
+  int n_obs;
+};
+
+struct TorqueCfg {
+  int mode;      // 0 base, 1 nov, 2 rne
+  double mass;   // problem.payload_mass
+};
+
+// ------------------------------------------------------------------------------------------
+// utils.py closures
+// ------------------------------------------------------------------------------------------
+// get_refine_fn step (utils.py:3037): q <- (1/(n-i)) * (q2 - q) + q.  No FMA contraction so
+// the intermediate edge points match numpy bit for bit.
+__device__ __forceinline__ void refine_step(double q[7], const double q2[7], int n, int i) {
+#pragma clang fp contract(off)
+  const double r = 1.0 / (double)(n - i);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) q[k] = r * (q2[k] - q[k]) + q[k];
+}
+
+// int(norm(diff / resolution, 2)) + 1 (utils.py:3072 + refine num_steps+1)
+__device__ __forceinline__ int num_steps(const double q1[7], const double q2[7],
+                                         const double res[7]) {
+#pragma clang fp contract(off)
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double x = (q2[k] - q1[k]) / res[k];
+    s += x * x;
+  }
+  const double r = sqrt(s);
+  // bounded so a corrupt input can never spin a lane forever
+  return (r < 1048576.0) ? (int)r + 1 : 1048577;
+}
+
+// sqrt(dot(w, diff*diff)) (utils.py:3010-3017)
+__device__ __forceinline__ double distance(const double a[7], const double b[7],
+                                           const double w[7]) {
+#pragma clang fp contract(off)
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double d = b[k] - a[k];
+    s += w[k] * (d * d);
+  }
+  return sqrt(s);
+}
+
+__device__ __forceinline__ bool limits_violated(const double q[7]) {
+  bool bad = false;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) bad |= !(kLo[k] <= q[k]) || !(q[k] <= kHi[k]);
+  return bad;
+}
+
+// ------------------------------------------------------------------------------------------
+// rne.py: recursive Newton-Euler, 7 links + composite (flange, hand, payload) body.
+// The reference builds 6x6 spatial matrices per body (rne.py:9-27, 216-251); this is the
+// same recursion written on 3-vectors with the Panda's bodies 8..10 merged (identity
+// transforms, zero joint rates between them), identical up to rounding.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void cross3(const double a[3], const double b[3], double o[3]) {
+  o[0] = a[1] * b[2] - a[2] * b[1];
+  o[1] = a[2] * b[0] - a[0] * b[2];
+  o[2] = a[0] * b[1] - a[1] * b[0];
+}
+
+// R^T x for the DH rotation of row j (rows of tf_mat, rne.py:39-42)
+__device__ __forceinline__ void dh_rt(int j, double c, double s, const double x[3], double o[3]) {
+  const double ca = kDhCa[j], sa = kDhSa[j];
+  // R = [[c, -s, 0], [s ca, c ca, -sa], [s sa, c sa, ca]]
+  o[0] = c * x[0] + (s * ca) * x[1] + (s * sa) * x[2];
+  o[1] = -s * x[0] + (c * ca) * x[1] + (c * sa) * x[2];
+  o[2] = -sa * x[1] + ca * x[2];
+}
+__device__ __forceinline__ void dh_r(int j, double c, double s, const double x[3], double o[3]) {
+  const double ca = kDhCa[j], sa = kDhSa[j];
+  o[0] = c * x[0] - s * x[1];
+  o[1] = (s * ca) * x[0] + (c * ca) * x[1] - sa * x[2];
+  o[2] = (s * sa) * x[0] + (c * sa) * x[1] + ca * x[2];
+}
+
+// tau[7] = rne(q, qd, qdd) with payload mass mp (0 = no payload).  cq/sq = cos/sin(q).
+template <bool DYN>
+__device__ __forceinline__ void rne(const double cq[7], const double sq[7], const double qd[7],
+                                    const double qdd[7], double mp, double tau[7]) {
+  double w[3] = {0, 0, 0}, v[3] = {0, 0, 0}, al[3] = {0, 0, 0}, ac[3] = {0, 0, 9.81};
+  double fl[8][3], fa[8][3];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const double c = i < 7 ? cq[i] : 1.0, s = i < 7 ? sq[i] : 0.0;
+    const double p[3] = {kDhA[i], -kDhSa[i] * kDhD[i], kDhCa[i] * kDhD[i]};
+    double wn[3], vn[3], aln[3], acn[3];
+    if (DYN) {
+      double t[3], u[3];
+      cross3(w, p, t);
+      u[0] = v[0] + t[0]; u[1] = v[1] + t[1]; u[2] = v[2] + t[2];
+      dh_rt(i, c, s, u, vn);
+      double Ew[3];
+      dh_rt(i, c, s, w, Ew);
+      const double qdi = i < 7 ? qd[i] : 0.0, qddi = i < 7 ? qdd[i] : 0.0;
+      wn[0] = Ew[0]; wn[1] = Ew[1]; wn[2] = Ew[2] + qdi;
+      cross3(al, p, t);
+      u[0] = ac[0] + t[0]; u[1] = ac[1] + t[1]; u[2] = ac[2] + t[2];
+      dh_rt(i, c, s, u, acn);
+      // + v_i x (qd e_z)
+      acn[0] += vn[1] * qdi; acn[1] -= vn[0] * qdi;
+      dh_rt(i, c, s, al, aln);
+      // + (E w) x (qd e_z)
+      aln[0] += Ew[1] * qdi; aln[1] -= Ew[0] * qdi; aln[2] += qddi;
+    } else {
+      dh_rt(i, c, s, ac, acn);
+    }
+    // body forces f = I a + crf(v) I v
+    if (i < 7) {
+      const double m = kMass[i];
+      const double* cc = kCom[i];
+      const double* In = kInertia[i];
+      if (DYN) {
+        double t[3], vc[3], acc[3], hl[3], ha[3], Iw[3], Ial[3];
+        cross3(wn, cc, t);
+        vc[0] = vn[0] + t[0]; vc[1] = vn[1] + t[1]; vc[2] = vn[2] + t[2];
+        cross3(aln, cc, t);
+        acc[0] = acn[0] + t[0]; acc[1] = acn[1] + t[1]; acc[2] = acn[2] + t[2];
+        hl[0] = m * vc[0]; hl[1] = m * vc[1]; hl[2] = m * vc[2];
+        Iw[0] = In[0] * wn[0] + In[1] * wn[1] + In[2] * wn[2];
+        Iw[1] = In[1] * wn[0] + In[3] * wn[1] + In[4] * wn[2];
+        Iw[2] = In[2] * wn[0] + In[4] * wn[1] + In[5] * wn[2];
+        Ial[0] = In[0] * aln[0] + In[1] * aln[1] + In[2] * aln[2];
+        Ial[1] = In[1] * aln[0] + In[3] * aln[1] + In[4] * aln[2];
+        Ial[2] = In[2] * aln[0] + In[4] * aln[1] + In[5] * aln[2];
+        double cv[3], ca2[3];
+        cross3(cc, vc, cv);
+        cross3(cc, acc, ca2);
+        ha[0] = Iw[0] + m * cv[0]; ha[1] = Iw[1] + m * cv[1]; ha[2] = Iw[2] + m * cv[2];
+        double wxh[3], vxh[3], wxha[3];
+        cross3(wn, hl, wxh);
+        cross3(vn, hl, vxh);
+        cross3(wn, ha, wxha);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          fl[i][k] = m * acc[k] + wxh[k];
+          fa[i][k] = Ial[k] + m * ca2[k] + vxh[k] + wxha[k];
+        }
+      } else {
+        double ca2[3];
+        cross3(cc, acn, ca2);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          fl[i][k] = m * acn[k];
+          fa[i][k] = m * ca2[k];
+        }
+      }
+    } else {
+      // composite flange (m 0, I .001) + hand (m .68, I .1) + payload (m mp, I diag(mr^2,mr^2,0))
+      const double m = kHandMass + mp;
+      if (DYN) {
+        const double Ixy = kFlangeHandI + mp * (kPayloadR * kPayloadR), Iz = kFlangeHandI;
+        double hl[3] = {m * vn[0], m * vn[1], m * vn[2]};
+        double ha[3] = {Ixy * wn[0], Ixy * wn[1], Iz * wn[2]};
+        double wxh[3], vxh[3], wxha[3];
+        cross3(wn, hl, wxh);
+        cross3(vn, hl, vxh);
+        cross3(wn, ha, wxha);
+        fl[i][0] = m * acn[0] + wxh[0];
+        fl[i][1] = m * acn[1] + wxh[1];
+        fl[i][2] = m * acn[2] + wxh[2];
+        fa[i][0] = Ixy * aln[0] + vxh[0] + wxha[0];
+        fa[i][1] = Ixy * aln[1] + vxh[1] + wxha[1];
+        fa[i][2] = Iz * aln[2] + vxh[2] + wxha[2];
+      } else {
+        fl[i][0] = m * acn[0]; fl[i][1] = m * acn[1]; fl[i][2] = m * acn[2];
+        fa[i][0] = 0; fa[i][1] = 0; fa[i][2] = 0;
+      }
+    }
+    if (DYN) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) { w[k] = wn[k]; v[k] = vn[k]; al[k] = aln[k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 3; ++k) ac[k] = acn[k];
+  }
+  // backward pass (rne.py:247-251): f_{i-1} += Ad(Xup_i)^T f_i
+#pragma unroll
+  for (int i = 7; i >= 1; --i) {
+    const double c = i < 7 ? cq[i] : 1.0, s = i < 7 ? sq[i] : 0.0;
+    const double p[3] = {kDhA[i], -kDhSa[i] * kDhD[i], kDhCa[i] * kDhD[i]};
+    double Rf[3], Rn[3], pxRf[3];
+    dh_r(i, c, s, fl[i], Rf);
+    dh_r(i, c, s, fa[i], Rn);
+    cross3(p, Rf, pxRf);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      fl[i - 1][k] += Rf[k];
+      fa[i - 1][k] += pxRf[k] + Rn[k];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 7; ++i) tau[i] = fa[i][2];
+}
+
+// torque test: true = within limits (joint 7 unchecked, `>=` fails)
+template <bool DYN>
+__device__ __forceinline__ bool torque_ok(const double cq[7], const double sq[7],
+                                          const double qd[7], const double qdd[7],
+                                          double mass) {
+  double tau[7];
+  rne<DYN>(cq, sq, qd, qdd, mass > kPayloadMin ? mass : 0.0, tau);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) ok &= !(fabs(tau[i]) >= kEffort[i]);
+  return ok;
+}
+
+// ------------------------------------------------------------------------------------------
+// wave helpers
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int lane_id() { return __lane_id(); }
+
+__device__ __forceinline__ double wave_min(double x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = fmin(x, __shfl_xor(x, o));
+  return x;
+}
+__device__ __forceinline__ double wave_max(double x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x = fmax(x, __shfl_xor(x, o));
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------
+// exact hull-vs-box penetration depth, wave-cooperative (every lane of the wave calls it
+// with identical arguments).  Penetration = min over the facets of the Minkowski
+// difference: box faces, hull facets, silhouette hull edges x box axes (Gauss-map pruning).
+// R,p: link pose (world); ob: obstacle record.  Early-outs once < kPen (result only
+// compared against kPen).
+// ------------------------------------------------------------------------------------------
+struct Pose {
+  double R[9];
+  double p[3];
+};
+
+__device__ __noinline__ double exact_pd_wave(int link, const Pose pose,
+                                             const double* __restrict__ ob, const Geo g) {
+  const int lane = lane_id();
+  const double* R = pose.R;
+  const double* p = pose.p;
+  // box in the link frame
+  const double d[3] = {ob[0] - p[0], ob[1] - p[1], ob[2] - p[2]};
+  double cl[3], A[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = R[0 + i] * d[0] + R[3 + i] * d[1] + R[6 + i] * d[2];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A[3 * i + j] = R[0 + i] * ob[3 + j] + R[3 + i] * ob[6 + j] + R[6 + i] * ob[9 + j];
+  }
+  const double h[3] = {ob[12], ob[13], ob[14]};
+  const int v0 = tcmp_geo_vert_off[link], v1 = tcmp_geo_vert_off[link + 1];
+  const int f0 = tcmp_geo_plane_off[link], f1 = tcmp_geo_plane_off[link + 1];
+  const int e0 = tcmp_geo_edge_off[link], e1 = tcmp_geo_edge_off[link + 1];
+  // box face facets: hull support along +-a_i
+  double mn0 = INFINITY, mn1 = INFINITY, mn2 = INFINITY;
+  double mx0 = -INFINITY, mx1 = -INFINITY, mx2 = -INFINITY;
+  for (int v = v0 + lane; v < v1; v += 64) {
+    const double4 P = *reinterpret_cast<const double4*>(g.verts + 4 * v);
+    const double d0 = A[0] * P.x + A[3] * P.y + A[6] * P.z;
+    const double d1 = A[1] * P.x + A[4] * P.y + A[7] * P.z;
+    const double d2 = A[2] * P.x + A[5] * P.y + A[8] * P.z;
+    mn0 = fmin(mn0, d0); mx0 = fmax(mx0, d0);
+    mn1 = fmin(mn1, d1); mx1 = fmax(mx1, d1);
+    mn2 = fmin(mn2, d2); mx2 = fmax(mx2, d2);
+  }
+  mn0 = wave_min(mn0); mn1 = wave_min(mn1); mn2 = wave_min(mn2);
+  mx0 = wave_max(mx0); mx1 = wave_max(mx1); mx2 = wave_max(mx2);
+  double pd = INFINITY;
+  {
+    const double pc0 = A[0] * cl[0] + A[3] * cl[1] + A[6] * cl[2];
+    const double pc1 = A[1] * cl[0] + A[4] * cl[1] + A[7] * cl[2];
+    const double pc2 = A[2] * cl[0] + A[5] * cl[1] + A[8] * cl[2];
+    pd = fmin(pd, fmin(mx0 - pc0 + h[0], pc0 + h[0] - mn0));
+    pd = fmin(pd, fmin(mx1 - pc1 + h[1], pc1 + h[1] - mn1));
+    pd = fmin(pd, fmin(mx2 - pc2 + h[2], pc2 + h[2] - mn2));
+  }
+  if (pd < kPen) return pd;
+  double loc = INFINITY;
+  // hull facets
+  for (int f = f0 + lane; f < f1; f += 64) {
+    const double* P = g.planes + 8 * f;
+    const double4 n = *reinterpret_cast<const double4*>(P);
+    const double wmin = P[4];
+    (void)wmin;
+    const double pc = n.x * cl[0] + n.y * cl[1] + n.z * cl[2];
+    const double rad = h[0] * fabs(n.x * A[0] + n.y * A[3] + n.z * A[6]) +
+                       h[1] * fabs(n.x * A[1] + n.y * A[4] + n.z * A[7]) +
+                       h[2] * fabs(n.x * A[2] + n.y * A[5] + n.z * A[8]);
+    loc = fmin(loc, n.w - pc + rad);
+  }
+  // silhouette edges x box axes
+  for (int e = e0 + lane; e < e1; e += 64) {
+    const double* E = g.edges + 16 * e;
+    const double4 ev = *reinterpret_cast<const double4*>(E);
+    const double4 va = *reinterpret_cast<const double4*>(E + 4);
+    const double4 n1 = *reinterpret_cast<const double4*>(E + 8);
+    const double4 n2 = *reinterpret_cast<const double4*>(E + 12);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double ax0 = A[0 + i], ax1 = A[3 + i], ax2 = A[6 + i];
+      const double s1 = n1.x * ax0 + n1.y * ax1 + n1.z * ax2;
+      const double s2 = n2.x * ax0 + n2.y * ax1 + n2.z * ax2;
+      if (s1 * s2 < 0) {
+        double m0 = ev.y * ax2 - ev.z * ax1, m1 = ev.z * ax0 - ev.x * ax2,
+               m2 = ev.x * ax1 - ev.y * ax0;
+        const double len2 = m0 * m0 + m1 * m1 + m2 * m2;
+        if (len2 >= 1e-24) {
+          if (m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z) < 0) {
+            m0 = -m0; m1 = -m1; m2 = -m2;
+          }
+          const double hv = m0 * va.x + m1 * va.y + m2 * va.z;
+          const double pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
+          const double rad = h[0] * fabs(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
+                             h[1] * fabs(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
+                             h[2] * fabs(m0 * A[2] + m1 * A[5] + m2 * A[8]);
+          loc = fmin(loc, (hv - pc + rad) / sqrt(len2));
+        }
+      }
+    }
+  }
+  return fmin(pd, wave_min(loc));
+}
+
+// ------------------------------------------------------------------------------------------
+// configuration check: collision (limits + 10 links x obstacles) and torque test.
+// MUST be called by every lane of the wave (uniform control flow); `active` masks lanes.
+// Collision tiers per (link, obstacle): (1) link-OBB extent on the obstacle's axes < pen ->
+// free; (2) outer-OBB SAT < pen -> free; (3) inner-box SAT >= pen -> collision;
+// (4) otherwise the exact wave-cooperative hull test.  (1)-(3) are conservative bounds of
+// (4) (inner box subset hull subset outer OBB), so the answer is exactly (4)'s.
+// ------------------------------------------------------------------------------------------
+struct StepStats {
+  unsigned pairs_tested;  // tier-1 tests
+  unsigned pairs_sat;     // tier-2/3 evaluations
+  unsigned pairs_exact;   // tier-4 evaluations (wave-level count, lane 0)
+};
+
+__device__ __forceinline__ void frame_step(double R[9], double p[3], const double Rl[9],
+                                           const double t[3]) {
+  double nR[9], np[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      nR[3 * i + j] = R[3 * i + 0] * Rl[0 + j] + R[3 * i + 1] * Rl[3 + j] + R[3 * i + 2] * Rl[6 + j];
+    np[i] = R[3 * i + 0] * t[0] + R[3 * i + 1] * t[1] + R[3 * i + 2] * t[2] + p[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = nR[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = np[k];
+}
+
+// classify one (link, obstacle) pair with the link pose (R, p):
+// 0 free, 1 collision, 2 undecided (needs the exact test)
+__device__ __forceinline__ int classify_pair(int link, const double R[9], const double p[3],
+                                             const double wc[3], const double U[9],
+                                             const double aabb[3],
+                                             const double* __restrict__ ob, StepStats& st) {
+  const double* bx = tcmp_geo_boxes + 18 * link;
+  const double h0 = ob[12], h1 = ob[13], h2 = ob[14];
+  const bool aligned = ob[15] != 0.0;
+  // tier 1: link OBB extent along the obstacle axes
+  double dc[3] = {wc[0] - ob[0], wc[1] - ob[1], wc[2] - ob[2]};
+  st.pairs_tested++;
+  if (aligned) {
+    if ((h0 + aabb[0]) - fabs(dc[0]) < kPen) return 0;
+    if ((h1 + aabb[1]) - fabs(dc[1]) < kPen) return 0;
+    if ((h2 + aabb[2]) - fabs(dc[2]) < kPen) return 0;
+  } else {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const double bk0 = ob[3 + k], bk1 = ob[6 + k], bk2 = ob[9 + k];
+      const double dk = bk0 * dc[0] + bk1 * dc[1] + bk2 * dc[2];
+      double r = 0;
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+        r += bx[12 + i] * fabs(bk0 * U[0 + i] + bk1 * U[3 + i] + bk2 * U[6 + i]);
+      if ((ob[12 + k] + r) - fabs(dk) < kPen) return 0;
+    }
+  }
+  st.pairs_sat++;
+  // tiers 2/3: 15-axis SAT in the link-box frame (M = U^T B, t = U^T (c - w))
+  double M[9], aM[9], t[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    t[i] = -(U[0 + i] * dc[0] + U[3 + i] * dc[1] + U[6 + i] * dc[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      M[3 * i + j] = U[0 + i] * ob[3 + j] + U[3 + i] * ob[6 + j] + U[6 + i] * ob[9 + j];
+      aM[3 * i + j] = fabs(M[3 * i + j]);
+    }
+  }
+  const double oh[3] = {bx[12], bx[13], bx[14]};
+  const double ih[3] = {bx[15], bx[16], bx[17]};
+  const double hb[3] = {h0, h1, h2};
+  bool inner_all = ih[0] > 0.0;
+  constexpr double P2 = kPen * kPen;
+  // link box axes
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const double rb = hb[0] * aM[3 * i + 0] + hb[1] * aM[3 * i + 1] + hb[2] * aM[3 * i + 2];
+    const double dist = fabs(t[i]);
+    if (oh[i] + rb - dist < kPen) return 0;
+    inner_all &= (ih[i] + rb - dist >= kPen);
+  }
+  // obstacle axes
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double ra = oh[0] * aM[j] + oh[1] * aM[3 + j] + oh[2] * aM[6 + j];
+    const double ri = ih[0] * aM[j] + ih[1] * aM[3 + j] + ih[2] * aM[6 + j];
+    const double dist = fabs(t[0] * M[j] + t[1] * M[3 + j] + t[2] * M[6 + j]);
+    if (ra + hb[j] - dist < kPen) return 0;
+    inner_all &= (ri + hb[j] - dist >= kPen);
+  }
+  // cross axes U_i x B_j, |n|^2 = 1 - M_ij^2
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int i1 = (i + 1) % 3, i2 = (i + 2) % 3;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int j1 = (j + 1) % 3, j2 = (j + 2) % 3;
+      const double n2 = 1.0 - M[3 * i + j] * M[3 * i + j];
+      if (n2 < 1e-12) continue;
+      const double ra = oh[i1] * aM[3 * i2 + j] + oh[i2] * aM[3 * i1 + j];
+      const double ri = ih[i1] * aM[3 * i2 + j] + ih[i2] * aM[3 * i1 + j];
+      const double rb = hb[j1] * aM[3 * i + j2] + hb[j2] * aM[3 * i + j1];
+      const double dist = fabs(t[i2] * M[3 * i1 + j] - t[i1] * M[3 * i2 + j]);
+      const double ov = ra + rb - dist;
+      if (ov < 0 || ov * ov < P2 * n2) return 0;
+      const double oi = ri + rb - dist;
+      inner_all &= (oi >= 0 && oi * oi >= P2 * n2);
+    }
+  }
+  return inner_all ? 1 : 2;
+}
+
+// world frames of the 10 collision links are generated incrementally; `fn(link, R, p)` is
+// invoked in link order with uniform control flow.
+template <typename F>
+__device__ __forceinline__ void for_each_link_frame(const double cq[7], const double sq[7], F&& fn) {
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
+    const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+    const double t[3] = {kJx[j], kJy[j], kJz[j]};
+    frame_step(R, p, Rl, t);
+    fn(j, R, p);
+  }
+  {
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double tz[3] = {0, 0, kFlangeZ};
+    frame_step(R, p, I, tz);
+    const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
+    const double z0[3] = {0, 0, 0};
+    frame_step(R, p, Rz, z0);
+    fn(7, R, p);
+    double Rf[9], pf[3];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Rf[k] = R[k];
+    const double tl[3] = {0, kFingerOpen, kFingerZ};
+    pf[0] = p[0]; pf[1] = p[1]; pf[2] = p[2];
+    frame_step(Rf, pf, I, tl);
+    fn(8, Rf, pf);
+    const double tr[3] = {0, -kFingerOpen, kFingerZ};
+    frame_step(R, p, I, tr);
+    fn(9, R, p);
+  }
+}
+
+// Returns collision flag; all lanes must call.  `active` lanes only contribute.
+__device__ __forceinline__ bool collides_wave(const double q[7], const double cq[7],
+                                              const double sq[7], bool active,
+                                              const Scene sc, const Geo g, StepStats& st) {
+  bool coll = active && limits_violated(q);
+  if (sc.n_obs == 0) return coll;
+  const int lane = lane_id();
+  for_each_link_frame(cq, sq, [&](int link, const double R[9], const double p[3]) {
+    // stop once no active lane is still free (uniform test)
+    if (__ballot(active && !coll) == 0) return;
+    const double* bx = tcmp_geo_boxes + 18 * link;
+    double wc[3], U[9], aabb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      wc[i] = R[3 * i + 0] * bx[0] + R[3 * i + 1] * bx[1] + R[3 * i + 2] * bx[2] + p[i];
+#pragma unroll
+      for (int j = 0; j < 3; ++j)
+        U[3 * i + j] = R[3 * i + 0] * bx[3 + j] + R[3 * i + 1] * bx[6 + j] + R[3 * i + 2] * bx[9 + j];
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+      aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
+    for (int o = 0; o < sc.n_obs; ++o) {
+      const double* __restrict__ ob = sc.obs + 16 * o;
+      int cls = 0;
+      if (active && !coll) cls = classify_pair(link, R, p, wc, U, aabb, ob, st);
+      coll |= (cls == 1);
+      uint64_t pend = __ballot(cls == 2);
+      while (pend) {
+        const int L = __builtin_ctzll(pend);
+        Pose PL;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) PL.p[k] = __shfl(p[k], L);
+        const double pd = exact_pd_wave(link, PL, ob, g);
+        if (lane == L) {
+          coll |= (pd >= kPen);
+          st.pairs_exact++;
+        }
+        pend &= pend - 1;
+      }
+    }
+  });
+  return coll;
+}
+
+// ------------------------------------------------------------------------------------------
+// Philox4x32-10 sample stream (same definition as oracle/tcmp_oracle.c)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void philox_uniforms(uint64_t seed, uint64_t k, double u[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    uint32_t c0 = (uint32_t)k, c1 = (uint32_t)(k >> 32), c2 = (uint32_t)j, c3 = 0x7463u;
+    uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+      const uint64_t p0 = (uint64_t)0xD2511F53u * c0;
+      const uint64_t p1 = (uint64_t)0xCD9E8D57u * c2;
+      const uint32_t hi0 = (uint32_t)(p0 >> 32), lo0 = (uint32_t)p0;
+      const uint32_t hi1 = (uint32_t)(p1 >> 32), lo1 = (uint32_t)p1;
+      const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+      c0 = n0; c1 = lo1; c2 = n2; c3 = lo0;
+      k0 += 0x9E3779B9u; k1 += 0xBB67AE85u;
+    }
+    const uint64_t a = ((uint64_t)c0 << 32) | c1, b = ((uint64_t)c2 << 32) | c3;
+    u[2 * j] = (double)(a >> 11) * 0x1.0p-53;
+    u[2 * j + 1] = (double)(b >> 11) * 0x1.0p-53;
+  }
+}
+
+}  // namespace tcmp

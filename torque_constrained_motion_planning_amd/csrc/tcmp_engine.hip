@@ -1,0 +1,1416 @@
+// tcmp_engine.hip -- MI355X (gfx950) engine for the torque-constrained RRT* hot path and its
+// C-ABI (include/tcmp.h).
+//
+// Reference path replaced: rrt_star.py:151-211 (rrt_star_force_aware) with its callbacks
+// utils.py:2985-3218 (sample/distance/extend/collision), panda_primitives.py:13-193,295-318
+// (torque tests, dynam_fn), rne.py:198-254, min_jerk_v2.py:80-222.
+//
+// Round structure (batched frontier, B candidates per round, one HIP stream):
+//   k_sample        Philox4x32-10 candidate draws (or host-provided draws)
+//   k_nearest       LDS-tiled brute-force argmin over the tree snapshot (fp64 VALU bound)
+//   k_edges         persistent lane-refill edge walker: extend steps, collision, torque
+//   k_insert        lane-ordered insertion (block scan), goal test
+//   k_rewire_scan   neighbours within radius of each new node (snapshot)
+//   k_rewire_apply  sequential rewire per new node (rrt_star.py:187-192)
+// then k_retrace / k_traj (min-jerk + final dynamic torque validation).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <climits>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "tcmp_device.h"
+#include "../../include/tcmp.h"
+
+using namespace tcmp;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIPCHK(x)                                                                      \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      return fail(-2, std::string(#x) + ": " + hipGetErrorString(e_));                 \
+  } while (0)
+
+constexpr int kNbrCap = 8;     // stored rewire neighbours per new node
+constexpr int kNnTile = 256;   // tree nodes per LDS tile
+constexpr int kNnCpt = 2;      // candidates per thread in k_nearest
+
+struct DevState {
+  long long n_nodes;
+  long long snap;
+  long long new_count;
+  long long goal_node;
+  long long samples;
+  long long W, ni, K, first_fail;
+  unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
+  int work_counter;
+  int round_goal;
+  int status;
+  int overflow;
+};
+
+struct PlanParams {
+  double start[7], goal[7], w[7], res[7];
+  double radius, goal_prob, goal_tol, mass, exec_time;
+  unsigned long long seed;
+  int torque_mode;
+  int uniform_w;
+  long long max_nodes;
+};
+
+struct Tree {
+  double* cfg;     // [N][8]: q0..q6, cost
+  int* parent;     // [N]
+  double* tgt;     // [N][8]: extend target q0..q6
+  int2* meta;      // [N]: (n_steps, n_safe)
+};
+
+__device__ __forceinline__ void load7(const double* p, double q[7]) {
+  const double4 a = *reinterpret_cast<const double4*>(p);
+  const double2 b = *reinterpret_cast<const double2*>(p + 4);
+  q[0] = a.x; q[1] = a.y; q[2] = a.z; q[3] = a.w; q[4] = b.x; q[5] = b.y; q[6] = p[6];
+}
+__device__ __forceinline__ void store7(double* p, const double q[7]) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) p[k] = q[k];
+}
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
+// ------------------------------------------------------------------------------------------
+// k_sample: uniform configurations (utils.py:2941-2990 convex_combination of the limits)
+// ------------------------------------------------------------------------------------------
+__global__ void k_sample(PlanParams P, DevState* st, long long base, int nb, double* cand,
+                         unsigned char* cgoal) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  const long long it = base + j;
+  double u[8];
+  philox_uniforms(P.seed, (uint64_t)it, u);
+  {
+#pragma clang fp contract(off)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = (1 - u[k]) * kLo[k] + u[k] * kHi[k];
+  }
+  cgoal[j] = 0;
+  const bool raw = st->goal_node < 0 && (it == 0 || u[7] < P.goal_prob);
+  if (raw) atomicMin(&st->round_goal, j);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_nearest: argmin_n sum_k w_k (s_k - n_k)^2 over the snapshot, ties -> lowest index.
+// Block = 256 threads x kNnCpt candidates; the tree streams through LDS in 256-node tiles
+// (16 KiB) that every lane reads by broadcast.
+// ------------------------------------------------------------------------------------------
+template <bool UW>
+__global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, const double* tree,
+                                                 long long T_override, double* cand,
+                                                 unsigned char* cgoal, int nb, int* nn,
+                                                 int device_sampled) {
+  __shared__ double4 tile[2 * kNnTile];
+  const int tid = threadIdx.x;
+  const long long T = T_override >= 0 ? T_override : st->n_nodes;
+  const int rg = device_sampled ? st->round_goal : INT_MAX;
+  double s[kNnCpt][7];
+  double best[kNnCpt];
+  int bi[kNnCpt];
+#pragma unroll
+  for (int c = 0; c < kNnCpt; ++c) {
+    const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
+    best[c] = INFINITY;
+    bi[c] = 0;
+    if (j < nb) {
+      if (j == rg) {  // the round's goal-biased lane (rrt_star.py:160-161)
+#pragma unroll
+        for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = P.goal[k];
+        cgoal[j] = 1;
+      }
+      load7(cand + 8 * (size_t)j, s[c]);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) s[c][k] = 0;
+    }
+  }
+  double w[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) w[k] = P.w[k];
+  const double4* t4 = reinterpret_cast<const double4*>(tree);
+  for (long long base = 0; base < T; base += kNnTile) {
+    const long long n = base + tid;
+    if (n < T) {
+      tile[2 * tid] = t4[2 * n];
+      tile[2 * tid + 1] = t4[2 * n + 1];
+    }
+    __syncthreads();
+    const int cnt = (int)min((long long)kNnTile, T - base);
+    for (int jj = 0; jj < cnt; ++jj) {
+      const double4 a = tile[2 * jj], b = tile[2 * jj + 1];
+#pragma unroll
+      for (int c = 0; c < kNnCpt; ++c) {
+        const double d0 = s[c][0] - a.x, d1 = s[c][1] - a.y, d2 = s[c][2] - a.z,
+                     d3 = s[c][3] - a.w, d4 = s[c][4] - b.x, d5 = s[c][5] - b.y,
+                     d6 = s[c][6] - b.z;
+        double dd;
+        if (UW) {
+          dd = d0 * d0;
+          dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
+          dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
+        } else {
+          dd = w[0] * (d0 * d0);
+          dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
+          dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
+        }
+        if (dd < best[c]) {
+          best[c] = dd;
+          bi[c] = (int)(base + jj);
+        }
+      }
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int c = 0; c < kNnCpt; ++c) {
+    const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
+    if (j < nb) nn[j] = bi[c];
+  }
+  if (blockIdx.x == 0 && tid == 0) atomicAdd(&st->nn_pairs, (unsigned long long)nb * (unsigned long long)T);
+}
+
+// ------------------------------------------------------------------------------------------
+// k_edges: safe_path_force_aware(extend(from, to)) for n edges (rrt_star.py:90-98).
+// Persistent: each lane walks one edge step by step; a lane whose edge ends (first failing
+// step or last step) takes the next edge from a global queue (one atomic per wave), so
+// lanes never idle behind the longest edge of their wave.
+// ------------------------------------------------------------------------------------------
+struct EdgeJob {
+  const double* from_base;  // stride 8
+  const int* from_idx;      // nullable: from = from_base[from_idx[e]]
+  const double* to;         // stride 8
+  int n;
+  int* nsafe;
+  int* nsteps;
+  double* last;             // stride 8
+};
+
+__global__ __launch_bounds__(256) void k_edges(EdgeJob J, PlanParams P, Scene sc, Geo g,
+                                               DevState* st) {
+  const int lane = lane_id();
+  int e = -1, i = 0, n = 0;
+  bool done = false;
+  double q[7], q2[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) { q[k] = 0.5 * (kLo[k] + kHi[k]); q2[k] = q[k]; }
+  StepStats ss = {0, 0, 0};
+  unsigned long long steps = 0;
+  double res[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) res[k] = P.res[k];
+  while (true) {
+    const bool need = !done && e < 0;
+    const uint64_t m = __ballot(need);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&st->work_counter, (int)__popcll(m));
+      base = __shfl(base, leader);
+      if (need) {
+        const int my = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+        if (my < J.n) {
+          e = my;
+          const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
+          load7(J.from_base + 8 * src, q);
+          load7(J.to + 8 * (size_t)e, q2);
+          n = num_steps(q, q2, res);
+          i = 0;
+        } else {
+          done = true;
+        }
+      }
+    }
+    if (__ballot(!done) == 0) break;
+    const bool active = e >= 0;
+    double qn[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) qn[k] = q[k];
+    if (active) refine_step(qn, q2, n, i);
+    double cq[7], sq[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
+    const bool coll = collides_wave(qn, cq, sq, active, sc, g, ss);
+    bool ok = active && !coll;
+    if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
+      const double z[7] = {0, 0, 0, 0, 0, 0, 0};
+      ok = torque_ok<false>(cq, sq, z, z, P.mass);
+    }
+    if (active) {
+      ++steps;
+      if (ok) {
+#pragma unroll
+        for (int k = 0; k < 7; ++k) q[k] = qn[k];
+        ++i;
+      }
+      if (!ok || i == n) {
+        J.nsafe[e] = i;
+        J.nsteps[e] = n;
+        store7(J.last + 8 * (size_t)e, q);
+        e = -1;
+      }
+    }
+  }
+  const unsigned long long a = wave_sum_u64(steps), b = wave_sum_u64(ss.pairs_tested),
+                           c = wave_sum_u64(ss.pairs_sat), d = wave_sum_u64(ss.pairs_exact);
+  if (lane == 0) {
+    atomicAdd(&st->edge_steps, a);
+    atomicAdd(&st->pairs_tested, b);
+    atomicAdd(&st->pairs_sat, c);
+    atomicAdd(&st->pairs_exact, d);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_insert: lane-ordered insertion of accepted edges (rrt_star.py:173-180), one block.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tree tr,
+                                                 const int* nn, const double* cand,
+                                                 const unsigned char* cgoal, const int* nsafe,
+                                                 const int* nsteps, const double* last, int nb) {
+  __shared__ int scan[1024];
+  __shared__ long long gbest[1024];
+  const int tid = threadIdx.x;
+  const long long T = st->n_nodes;
+  const bool goal_open = st->goal_node < 0;
+  const int chunk = (nb + 1023) / 1024;
+  const int j0 = min(nb, tid * chunk), j1 = min(nb, j0 + chunk);
+  int cnt = 0;
+  for (int j = j0; j < j1; ++j) cnt += nsafe[j] > 0;
+  scan[tid] = cnt;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int v = tid >= o ? scan[tid - o] : 0;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const int total = scan[1023];
+  long long idx = T + scan[tid] - cnt;
+  long long best = LLONG_MAX;
+  const bool fits = T + total <= P.max_nodes;
+  if (fits) {
+    for (int j = j0; j < j1; ++j) {
+      if (nsafe[j] <= 0) continue;
+      const int par = nn[j];
+      double pc[7], lq[7], tq[7];
+      load7(tr.cfg + 8 * (size_t)par, pc);
+      load7(last + 8 * (size_t)j, lq);
+      load7(cand + 8 * (size_t)j, tq);
+      const double d = distance(pc, lq, P.w);
+      double* dst = tr.cfg + 8 * idx;
+      store7(dst, lq);
+      dst[7] = tr.cfg[8 * (size_t)par + 7] + d;
+      tr.parent[idx] = par;
+      store7(tr.tgt + 8 * idx, tq);
+      tr.meta[idx] = make_int2(nsteps[j], nsafe[j]);
+      if (goal_open && cgoal[j] && distance(lq, P.goal, P.w) < P.goal_tol) best = min(best, idx);
+      ++idx;
+    }
+  }
+  gbest[tid] = best;
+  __syncthreads();
+  for (int o = 512; o >= 1; o >>= 1) {
+    if (tid < o) gbest[tid] = min(gbest[tid], gbest[tid + o]);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    st->snap = T;
+    if (!fits) {
+      st->overflow = 1;
+      st->new_count = 0;
+    } else {
+      st->new_count = total;
+      st->n_nodes = T + total;
+      if (goal_open && gbest[0] != LLONG_MAX) st->goal_node = gbest[0];
+    }
+    st->samples += nb;
+    st->round_goal = INT_MAX;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// rewire (rrt_star.py:183-192): neighbours of each new node within `radius` among the
+// round's snapshot, visited in index order; reparent when cheaper and the edge is safe.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st, Tree tr,
+                                                     int* nbr, int* ncount) {
+  __shared__ double4 tile[2 * kNnTile];
+  const int tid = threadIdx.x;
+  const long long A = st->new_count, T = st->snap;
+  if ((long long)blockIdx.x * 256 >= A) return;  // block-uniform
+  const long long t = (long long)blockIdx.x * 256 + tid;
+  const bool act = t < A;
+  double qn[7];
+  if (act) load7(tr.cfg + 8 * (T + t), qn);
+  else for (int k = 0; k < 7; ++k) qn[k] = 1e30;
+  const double r2 = P.radius * P.radius;
+  int c = 0;
+  const double4* t4 = reinterpret_cast<const double4*>(tr.cfg);
+  for (long long base = 0; base < T; base += kNnTile) {
+    const long long n = base + tid;
+    if (n < T) {
+      tile[2 * tid] = t4[2 * n];
+      tile[2 * tid + 1] = t4[2 * n + 1];
+    }
+    __syncthreads();
+    const int cnt = (int)min((long long)kNnTile, T - base);
+    for (int jj = 0; jj < cnt; ++jj) {
+      const double4 a = tile[2 * jj], b = tile[2 * jj + 1];
+      const double d0 = qn[0] - a.x, d1 = qn[1] - a.y, d2 = qn[2] - a.z, d3 = qn[3] - a.w,
+                   d4 = qn[4] - b.x, d5 = qn[5] - b.y, d6 = qn[6] - b.z;
+      double dd = P.w[0] * (d0 * d0);
+      dd = fma(P.w[1] * d1, d1, dd); dd = fma(P.w[2] * d2, d2, dd); dd = fma(P.w[3] * d3, d3, dd);
+      dd = fma(P.w[4] * d4, d4, dd); dd = fma(P.w[5] * d5, d5, dd); dd = fma(P.w[6] * d6, d6, dd);
+      if (dd < r2 * 1.000001) {
+        const double nq[7] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z};
+        if (distance(nq, qn, P.w) < P.radius) {
+          if (c < kNbrCap) nbr[t * kNbrCap + c] = (int)(base + jj);
+          ++c;
+        }
+      }
+    }
+    __syncthreads();
+  }
+  if (act) ncount[t] = c;
+}
+
+__global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st, Tree tr,
+                                                      const int* nbr, const int* ncount,
+                                                      Scene sc, Geo g) {
+  const long long A = st->new_count, T = st->snap;
+  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = t < A && ncount[t] > 0;
+  if (__ballot(act) == 0) return;  // wave-uniform
+  const long long me = T + t;
+  double qn[7];
+  double cost_new = 0;
+  int cnt = 0;
+  if (act) {
+    load7(tr.cfg + 8 * me, qn);
+    cost_new = tr.cfg[8 * me + 7];
+    cnt = ncount[t];
+  } else {
+    for (int k = 0; k < 7; ++k) qn[k] = 0.5 * (kLo[k] + kHi[k]);
+  }
+  StepStats ss = {0, 0, 0};
+  int c = 0;
+  int prev = -1;
+  unsigned long long rew = 0;
+  while (true) {
+    // next neighbour in index order (stored list, then a serial rescan past the list)
+    int nidx = -1;
+    if (act && c < cnt) {
+      if (c < kNbrCap) {
+        nidx = nbr[t * kNbrCap + c];
+      } else {
+        for (long long n = prev + 1; n < T; ++n) {
+          double a[7];
+          load7(tr.cfg + 8 * n, a);
+          if (distance(a, qn, P.w) < P.radius) { nidx = (int)n; break; }
+        }
+      }
+    }
+    if (__ballot(nidx >= 0) == 0) break;
+    ++c;
+    if (nidx >= 0) prev = nidx;
+    double qs[7];
+    double d = 0, cn = 0;
+    bool alive = false;
+    int ns = 0, i = 0;
+    if (nidx >= 0) {
+      load7(tr.cfg + 8 * (size_t)nidx, qs);
+      cn = tr.cfg[8 * (size_t)nidx + 7];
+      d = distance(qs, qn, P.w);
+      alive = cn + d < cost_new;
+      ns = num_steps(qs, qn, P.res);
+    } else {
+      for (int k = 0; k < 7; ++k) qs[k] = qn[k];
+    }
+    const bool cond = alive;
+    double q[7];
+    for (int k = 0; k < 7; ++k) q[k] = qs[k];
+    while (__ballot(alive)) {
+      double qq[7];
+      for (int k = 0; k < 7; ++k) qq[k] = q[k];
+      if (alive) refine_step(qq, qn, ns, i);
+      double cq[7], sq[7];
+      for (int k = 0; k < 7; ++k) sincos(qq[k], &sq[k], &cq[k]);
+      const bool coll = collides_wave(qq, cq, sq, alive, sc, g, ss);
+      bool ok = alive && !coll;
+      if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
+        const double z[7] = {0, 0, 0, 0, 0, 0, 0};
+        ok = torque_ok<false>(cq, sq, z, z, P.mass);
+      }
+      if (alive) {
+        if (ok) {
+          for (int k = 0; k < 7; ++k) q[k] = qq[k];
+          ++i;
+          if (i == ns) alive = false;
+        } else {
+          alive = false;
+        }
+      }
+    }
+    if (cond && i > 0 && distance(qn, q, P.w) < 1e-6) {
+      // new.rewire(n, d, path[:-1]) (rrt_star.py:192, 47-58)
+      cost_new = cn + d;
+      tr.cfg[8 * me + 7] = cost_new;
+      tr.parent[me] = nidx;
+      store7(tr.tgt + 8 * me, qn);
+      tr.meta[me] = make_int2(ns, i);
+      ++rew;
+    }
+  }
+  const unsigned long long r = wave_sum_u64(rew);
+  if (lane_id() == 0 && r) atomicAdd(&st->rewires, r);
+}
+
+// ------------------------------------------------------------------------------------------
+// retrace (rrt_star.py:42-45, 202): [start] + for each edge root->goal the first n_safe-1
+// regenerated extend points + the node's configuration.  One block.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_retrace(PlanParams P, DevState* st, Tree tr,
+                                                 long long* chain, double* wp, long long wp_cap) {
+  __shared__ long long sL;
+  __shared__ long long part[256];
+  const int tid = threadIdx.x;
+  const long long goal = st->goal_node;
+  if (goal < 0) return;
+  if (tid == 0) {
+    long long L = 0;
+    const long long cap = st->n_nodes;
+    for (long long n = goal; n > 0 && L < cap; n = tr.parent[n]) chain[L++] = n;
+    sL = L;
+  }
+  __syncthreads();
+  const long long L = sL;
+  long long run = 1;  // waypoint 0 = start
+  for (long long b0 = 0; b0 < L; b0 += 256) {
+    const long long k = b0 + tid;  // root->goal order
+    long long node = -1;
+    long long cnt = 0;
+    if (k < L) {
+      node = chain[L - 1 - k];
+      cnt = tr.meta[node].y;
+    }
+    part[tid] = cnt;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {
+      const long long v = tid >= o ? part[tid - o] : 0;
+      __syncthreads();
+      part[tid] += v;
+      __syncthreads();
+    }
+    const long long off = run + part[tid] - cnt;
+    if (node >= 0 && off + cnt <= wp_cap) {
+      double q[7], tq[7];
+      load7(tr.cfg + 8 * (size_t)tr.parent[node], q);
+      load7(tr.tgt + 8 * node, tq);
+      const int2 mt = tr.meta[node];
+      for (int i = 0; i < mt.y - 1; ++i) {
+        refine_step(q, tq, mt.x, i);
+        store7(wp + 7 * (off + i), q);
+      }
+      double qn[7];
+      load7(tr.cfg + 8 * node, qn);
+      store7(wp + 7 * (off + mt.y - 1), qn);
+    }
+    run += part[255];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    double q0[7];
+    load7(tr.cfg, q0);
+    store7(wp, q0);
+    st->W = run;
+    if (run > wp_cap) { st->status = -3; return; }
+    // dynam_fn: num_intervals = move_time * 1000 / len(path) (panda_primitives.py:308)
+    const long long ni = (long long)(P.exec_time * 1000.0 / (double)run);
+    st->ni = ni;
+    st->K = ni > 0 ? (run - 1) * ni : 0;
+    st->first_fail = -1;
+    if (ni <= 0) st->status = TCMP_PLAN_MINJERK_ASSERT;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// min-jerk sample i of a waypoint path (min_jerk_v2.py:80-222 with unit durations)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double gv_at(const double* wp, long long nseg, long long s, int k) {
+  // goal velocity of segment s (waypoint s+1), min_jerk_v2.py:109-118
+#pragma clang fp contract(off)
+  if (s >= nseg - 1) return 0.0;
+  const double v0 = (wp[7 * (s + 1) + k] - wp[7 * s + k]) / 1.0;
+  const double v1 = (wp[7 * (s + 2) + k] - wp[7 * (s + 1) + k]) / 1.0;
+  return (v0 * v1 >= 1e-10) ? 0.5 * (v0 + v1) : 0.0;
+}
+
+__device__ __forceinline__ void minjerk_sample(const double* wp, long long nwp, long long ni,
+                                               long long i, double x[7], double v[7],
+                                               double a[7]) {
+#pragma clang fp contract(off)
+  const long long nseg = nwp - 1;
+  const long long s = i / ni, j = i % ni;
+  const double interval = 1.0 / (double)ni;
+  double t;
+  if (ni > 1) {
+    const double step = (1.0 - interval) / (double)(ni - 1);
+    t = (j == ni - 1) ? 1.0 : ((double)j * step + interval);
+  } else {
+    t = 0.0 * (1.0 - interval) + interval;
+  }
+  const double t2 = pow(t, 2.0), t3 = pow(t, 3.0), t4 = pow(t, 4.0), t5 = pow(t, 5.0);
+  const double T = 1.0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double x0 = wp[7 * s + k];
+    const double v0 = s > 0 ? gv_at(wp, nseg, s - 1, k) : 0.0;
+    const double a0 = 0.0;
+    const double gx = wp[7 * (s + 1) + k];
+    const double gv = gv_at(wp, nseg, s, k);
+    const double ga = 0.0;
+    const double A = (gx - (x0 + v0 * T + (a0 / 2.0) * T * T)) / (T * T * T);
+    const double B = (gv - (v0 + a0 * T)) / (T * T);
+    const double C = (ga - a0) / T;
+    const double c0 = x0, c1 = v0, c2 = a0 / 2.0;
+    const double c3 = 10 * A - 4 * B + 0.5 * C;
+    const double c4 = (-15 * A + 7 * B - C) / T;
+    const double c5 = (6 * A - 3 * B + 0.5 * C) / (T * T);
+    x[k] = c0 + c1 * t + c2 * t2 + c3 * t3 + c4 * t4 + c5 * t5;
+    v[k] = c1 + 2 * c2 * t + 3 * c3 * t2 + 4 * c4 * t3 + 5 * c5 * t4;
+    a[k] = 2 * c2 + 6 * c3 * t + 12 * c4 * t2 + 20 * c5 * t3;
+  }
+}
+
+__device__ __forceinline__ bool torque_test_sample(int mode, double mass, const double q[7],
+                                                   const double qd[7], const double qdd[7]) {
+  if (mode == TCMP_TORQUE_BASE) return true;
+  double cq[7], sq[7];
+  for (int k = 0; k < 7; ++k) sincos(q[k], &sq[k], &cq[k]);
+  if (mode == TCMP_TORQUE_NOV) {
+    const double z[7] = {0, 0, 0, 0, 0, 0, 0};
+    return torque_ok<false>(cq, sq, z, z, mass);
+  }
+  return torque_ok<true>(cq, sq, qd, qdd, mass);
+}
+
+// dynam_fn + final validation + Conf.torques for the planner's path (grid-stride)
+__global__ __launch_bounds__(256) void k_traj(PlanParams P, DevState* st, const double* wp,
+                                              double* oq, double* oqd, double* oqdd,
+                                              double* opsg, double* otau) {
+  if (st->status != 0 && st->status != TCMP_PLAN_VALIDATION_FAILED) return;
+  const long long K = st->K, ni = st->ni, W = st->W;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < K;
+       i += (long long)gridDim.x * blockDim.x) {
+    double x[7], v[7], a[7];
+    minjerk_sample(wp, W, ni, i, x, v, a);
+    store7(oq + 7 * i, x);
+    store7(oqd + 7 * i, v);
+    store7(oqdd + 7 * i, a);
+    {
+#pragma clang fp contract(off)
+      opsg[i] = (P.exec_time * (double)i) / (double)K;  // panda_primitives.py:315
+    }
+    if (!torque_test_sample(P.torque_mode, P.mass, x, v, a)) {
+      atomicMin(&st->first_fail, i);
+    }
+    double cq[7], sq[7], tau[7];
+    for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
+    rne<true>(cq, sq, v, a, 0.0, tau);  // Conf.torques: rne without payload (utils.py:3376)
+    store7(otau + 7 * i, tau);
+  }
+}
+
+// first_fail uses LLONG_MAX as "none" during the kernel
+__global__ void k_traj_prep(DevState* st) {
+  if (st->status == 0) st->first_fail = LLONG_MAX;
+}
+__global__ void k_traj_post(DevState* st) {
+  if (st->first_fail == LLONG_MAX) st->first_fail = -1;
+  else if (st->status == 0 && st->first_fail >= 0) st->status = TCMP_PLAN_VALIDATION_FAILED;
+}
+
+// ------------------------------------------------------------------------------------------
+// utility kernels behind the batched C-ABI entry points
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_check_configs(const double* q, long long n, Scene sc,
+                                                       Geo g, int* collides) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool act = i < n;
+  double x[7];
+  if (act) load7(q + 8 * i, x);
+  else for (int k = 0; k < 7; ++k) x[k] = 0.5 * (kLo[k] + kHi[k]);
+  double cq[7], sq[7];
+  for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
+  StepStats ss = {0, 0, 0};
+  const bool c = collides_wave(x, cq, sq, act, sc, g, ss);
+  if (act) collides[i] = c ? 1 : 0;
+}
+
+__global__ void k_torque(const double* q, const double* qd, const double* qdd, long long n,
+                         int mode, double mass, int* ok) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x[7], v[7], a[7];
+  load7(q + 8 * i, x);
+  if (qd) load7(qd + 8 * i, v); else for (int k = 0; k < 7; ++k) v[k] = 0;
+  if (qdd) load7(qdd + 8 * i, a); else for (int k = 0; k < 7; ++k) a[k] = 0;
+  ok[i] = torque_test_sample(mode, mass, x, v, a) ? 1 : 0;
+}
+
+__global__ void k_rne(const double* q, const double* qd, const double* qdd, long long n,
+                      double mp, double* tau) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x[7], v[7], a[7], cq[7], sq[7], t[7];
+  load7(q + 8 * i, x);
+  load7(qd + 8 * i, v);
+  load7(qdd + 8 * i, a);
+  for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
+  rne<true>(cq, sq, v, a, mp > 0 ? mp : 0.0, t);
+  store7(tau + 7 * i, t);
+}
+
+__global__ void k_minjerk(const double* wp, long long nwp, long long ni, double* oq, double* oqd,
+                          double* oqdd) {
+  const long long K = (nwp - 1) * ni;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < K;
+       i += (long long)gridDim.x * blockDim.x) {
+    double x[7], v[7], a[7];
+    minjerk_sample(wp, nwp, ni, i, x, v, a);
+    store7(oq + 7 * i, x);
+    store7(oqd + 7 * i, v);
+    store7(oqdd + 7 * i, a);
+  }
+}
+
+__global__ void k_validate(const double* q, const double* qd, const double* qdd, long long n,
+                           int mode, double mass, unsigned long long* first_fail, double* tau) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double x[7], v[7], a[7];
+  load7(q + 8 * i, x);
+  load7(qd + 8 * i, v);
+  load7(qdd + 8 * i, a);
+  if (!torque_test_sample(mode, mass, x, v, a)) atomicMin(first_fail, (unsigned long long)i);
+  if (tau) {
+    double cq[7], sq[7], t[7];
+    for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
+    rne<true>(cq, sq, v, a, 0.0, t);
+    store7(tau + 7 * i, t);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+template <typename T>
+struct DBuf {
+  T* p = nullptr;
+  size_t n = 0;
+  int ensure(size_t want) {
+    if (want <= n) return 0;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    hipError_t e = hipMalloc(&p, std::max<size_t>(want, 1) * sizeof(T));
+    if (e != hipSuccess) return fail(-2, std::string("hipMalloc: ") + hipGetErrorString(e));
+    n = want;
+    return 0;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_COUNT };
+
+struct EventPair {
+  hipEvent_t a, b;
+  int fam;
+};
+
+}  // namespace
+
+struct tcmp_handle {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int cu_count = 0;
+  DBuf<double> verts, planes, edges;
+  DBuf<double> obs;
+  int n_obs = 0;
+  DevState* st = nullptr;
+  // plan
+  PlanParams P{};
+  bool plan_open = false;
+  int max_batch = 0;
+  DBuf<double> cfg, tgt;
+  DBuf<int> parent;
+  DBuf<int2> meta;
+  DBuf<double> cand, last;
+  DBuf<unsigned char> cgoal;
+  DBuf<int> nn, nsafe, nsteps, nbr, ncount;
+  DBuf<long long> chain;
+  DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
+  long long samples_issued = 0;
+  // generic scratch
+  DBuf<double> s0, s1, s2, s3;
+  DBuf<int> i0, i1, i2;
+  DBuf<unsigned long long> u0;
+  // timing
+  std::vector<EventPair> ev_used;
+  std::vector<hipEvent_t> ev_pool;
+  double ms[F_COUNT] = {0, 0, 0, 0, 0};
+  long long launches_nearest = 0;
+  int edge_blocks = 0;
+
+  Geo geo() const { return Geo{verts.p, planes.p, edges.p}; }
+  Scene scene() const { return Scene{obs.p, n_obs}; }
+
+  hipEvent_t get_event() {
+    if (!ev_pool.empty()) {
+      hipEvent_t e = ev_pool.back();
+      ev_pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
+  }
+  void mark_begin(int fam, hipEvent_t* out) {
+    *out = get_event();
+    (void)hipEventRecord(*out, stream);
+    (void)fam;
+  }
+  void mark_end(int fam, hipEvent_t a) {
+    hipEvent_t b = get_event();
+    (void)hipEventRecord(b, stream);
+    ev_used.push_back(EventPair{a, b, fam});
+  }
+  void collect_events() {
+    for (auto& p : ev_used) {
+      float t = 0;
+      if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) ms[p.fam] += t;
+      ev_pool.push_back(p.a);
+      ev_pool.push_back(p.b);
+    }
+    ev_used.clear();
+  }
+};
+
+namespace {
+
+int set_dev(tcmp_handle* h) {
+  if (!h) return fail(-1, "null handle");
+  HIPCHK(hipSetDevice(h->device));
+  return 0;
+}
+
+// host rows of 7 -> device rows of 8
+int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
+  int rc = buf.ensure((size_t)n * 8);
+  if (rc) return rc;
+  std::vector<double> tmp((size_t)n * 8, 0.0);
+  for (long long i = 0; i < n; ++i)
+    for (int k = 0; k < 7; ++k) tmp[8 * i + k] = src[7 * i + k];
+  HIPCHK(hipMemcpyAsync(buf.p, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>(1, (n + block - 1) / block); }
+
+int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
+  if (J.n <= 0) return 0;
+  HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
+  // persistent grid: ~2 edges per lane keeps refill useful; bounded by residency
+  long long lanes = std::max<long long>(64, (J.n + 1) / 2);
+  long long blocks = (lanes + 255) / 256;
+  const long long cap = (long long)h->cu_count * 4;  // 4 x 256-thread blocks per CU
+  blocks = std::min(blocks, cap);
+  blocks = std::max<long long>(blocks, 1);
+  h->edge_blocks = (int)blocks;
+  hipLaunchKernelGGL(k_edges, dim3((unsigned)blocks), dim3(256), 0, h->stream, J, P,
+                     h->scene(), h->geo(), h->st);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+PlanParams default_params() {
+  PlanParams P{};
+  for (int k = 0; k < 7; ++k) {
+    P.w[k] = 10.0;
+    P.res[k] = 0.1;
+  }
+  P.radius = 0.01;
+  P.goal_prob = 0.2;
+  P.goal_tol = 1e-2;
+  P.uniform_w = 1;
+  P.max_nodes = LLONG_MAX;
+  return P;
+}
+
+}  // namespace
+
+// ==========================================================================================
+// C-ABI
+// ==========================================================================================
+extern "C" {
+
+const char* tcmp_last_error(void) { return g_err.c_str(); }
+int tcmp_version(void) { return 1; }
+
+int tcmp_device_count(int* n) {
+  if (!n) return fail(-1, "null");
+  HIPCHK(hipGetDeviceCount(n));
+  return 0;
+}
+
+int tcmp_create(int device, tcmp_handle** out) {
+  if (!out) return fail(-1, "null out");
+  *out = nullptr;
+  int nd = 0;
+  HIPCHK(hipGetDeviceCount(&nd));
+  if (device < 0 || device >= nd) return fail(-1, "device index out of range");
+  HIPCHK(hipSetDevice(device));
+  tcmp_handle* h = new tcmp_handle();
+  h->device = device;
+  hipDeviceProp_t prop;
+  HIPCHK(hipGetDeviceProperties(&prop, device));
+  h->cu_count = prop.multiProcessorCount;
+  HIPCHK(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  int rc = h->verts.ensure(TCMP_TOTAL_VERTS * 4);
+  rc = rc ? rc : h->planes.ensure(TCMP_TOTAL_PLANES * 8);
+  rc = rc ? rc : h->edges.ensure(TCMP_TOTAL_EDGES * 16);
+  if (rc) { delete h; return rc; }
+  HIPCHK(hipMemcpy(h->verts.p, tcmp_geo_verts, sizeof(tcmp_geo_verts), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->planes.p, tcmp_geo_planes, sizeof(tcmp_geo_planes), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(h->edges.p, tcmp_geo_edges, sizeof(tcmp_geo_edges), hipMemcpyHostToDevice));
+  HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
+  HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
+  *out = h;
+  return 0;
+}
+
+int tcmp_destroy(tcmp_handle* h) {
+  if (!h) return 0;
+  (void)hipSetDevice(h->device);
+  (void)hipStreamSynchronize(h->stream);
+  for (auto* b : {&h->verts, &h->planes, &h->edges, &h->obs, &h->cfg, &h->tgt, &h->cand,
+                  &h->last, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
+                  &h->s1, &h->s2, &h->s3})
+    b->release();
+  for (auto* b : {&h->parent, &h->nn, &h->nsafe, &h->nsteps, &h->nbr, &h->ncount, &h->i0,
+                  &h->i1, &h->i2})
+    b->release();
+  h->meta.release();
+  h->cgoal.release();
+  h->chain.release();
+  h->u0.release();
+  for (auto& p : h->ev_used) {
+    (void)hipEventDestroy(p.a);
+    (void)hipEventDestroy(p.b);
+  }
+  for (auto e : h->ev_pool) (void)hipEventDestroy(e);
+  if (h->st) (void)hipFree(h->st);
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+  return 0;
+}
+
+int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
+  if (int rc = set_dev(h)) return rc;
+  if (n_obs < 0 || (n_obs > 0 && !obb)) return fail(-1, "bad obstacle array");
+  std::vector<double> tmp((size_t)std::max(n_obs, 1) * 16, 0.0);
+  for (int o = 0; o < n_obs; ++o) {
+    const double* s = obb + 15 * o;
+    double* d = tmp.data() + 16 * o;
+    for (int k = 0; k < 15; ++k) d[k] = s[k];
+    const double* R = s + 3;
+    const bool aligned = R[0] == 1.0 && R[4] == 1.0 && R[8] == 1.0 && R[1] == 0.0 &&
+                         R[2] == 0.0 && R[3] == 0.0 && R[5] == 0.0 && R[6] == 0.0 &&
+                         R[7] == 0.0;
+    d[15] = aligned ? 1.0 : 0.0;
+    if (!(s[12] >= 0 && s[13] >= 0 && s[14] >= 0)) return fail(-1, "negative half extent");
+  }
+  if (int rc = h->obs.ensure(tmp.size())) return rc;
+  HIPCHK(hipMemcpyAsync(h->obs.p, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->n_obs = n_obs;
+  return 0;
+}
+
+int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                   int64_t n, double payload_mass, double* tau) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!q || !qd || !qdd || !tau))) return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, q, n);
+  rc = rc ? rc : upload7(h, h->s1, qd, n);
+  rc = rc ? rc : upload7(h, h->s2, qdd, n);
+  rc = rc ? rc : h->s3.ensure((size_t)n * 7);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_rne, dim3(grid_for(n, 128)), dim3(128), 0, h->stream, h->s0.p, h->s1.p,
+                     h->s2.p, (long long)n, payload_mass, h->s3.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(tau, h->s3.p, (size_t)n * 7 * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                   int64_t n, int32_t torque_mode, double payload_mass, int32_t* ok) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!q || !ok))) return fail(-1, "bad arguments");
+  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, q, n);
+  if (!rc && qd) rc = upload7(h, h->s1, qd, n);
+  if (!rc && qdd) rc = upload7(h, h->s2, qdd, n);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_torque, dim3(grid_for(n, 128)), dim3(128), 0, h->stream, h->s0.p,
+                     qd ? h->s1.p : nullptr, qdd ? h->s2.p : nullptr, (long long)n,
+                     (int)torque_mode, payload_mass, h->i0.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(ok, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* collides) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!q || !collides))) return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, q, n);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  if (rc) return rc;
+  hipLaunchKernelGGL(k_check_configs, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->s0.p,
+                     (long long)n, h->scene(), h->geo(), h->i0.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64_t n,
+                     const double* resolutions, int32_t torque_mode, double payload_mass,
+                     int32_t* n_safe, int32_t* n_steps, double* last) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || n > INT_MAX || (n > 0 && (!from || !to || !n_safe || !n_steps || !last)))
+    return fail(-1, "bad arguments");
+  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, from, n);
+  rc = rc ? rc : upload7(h, h->s1, to, n);
+  rc = rc ? rc : h->s2.ensure((size_t)n * 8);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  rc = rc ? rc : h->i1.ensure((size_t)n);
+  if (rc) return rc;
+  PlanParams P = default_params();
+  if (resolutions)
+    for (int k = 0; k < 7; ++k) P.res[k] = resolutions[k];
+  P.torque_mode = torque_mode;
+  P.mass = payload_mass;
+  EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p};
+  if ((rc = launch_edges(h, J, P))) return rc;
+  std::vector<double> tmp((size_t)n * 8);
+  HIPCHK(hipMemcpyAsync(n_safe, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(n_steps, h->i1.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(tmp.data(), h->s2.p, tmp.size() * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (long long i = 0; i < n; ++i)
+    for (int k = 0; k < 7; ++k) last[7 * i + k] = tmp[8 * i + k];
+  return 0;
+}
+
+int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* samples,
+                 int64_t n, const double* weights, int32_t* idx) {
+  if (int rc = set_dev(h)) return rc;
+  if (T <= 0 || n < 0 || n > INT_MAX || !tree || (n > 0 && (!samples || !idx)))
+    return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, tree, T);
+  rc = rc ? rc : upload7(h, h->s1, samples, n);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  rc = rc ? rc : h->cgoal.ensure((size_t)n);
+  if (rc) return rc;
+  PlanParams P = default_params();
+  bool uw = true;
+  if (weights) {
+    for (int k = 0; k < 7; ++k) {
+      P.w[k] = weights[k];
+      uw &= weights[k] == weights[0];
+    }
+  }
+  const unsigned grid = grid_for(n, 256 * kNnCpt);
+  if (uw)
+    hipLaunchKernelGGL(k_nearest<true>, dim3(grid), dim3(256), 0, h->stream, P, h->st, h->s0.p,
+                       (long long)T, h->s1.p, h->cgoal.p, (int)n, h->i0.p, 0);
+  else
+    hipLaunchKernelGGL(k_nearest<false>, dim3(grid), dim3(256), 0, h->stream, P, h->st, h->s0.p,
+                       (long long)T, h->s1.p, h->cgoal.p, (int)n, h->i0.p, 0);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_minjerk(tcmp_handle* h, const double* waypoints, int64_t n_wp, int64_t ni, double* q,
+                 double* qd, double* qdd) {
+  if (int rc = set_dev(h)) return rc;
+  if (ni <= 0) return fail(-1, "Invalid number of intervals chosen (must be greater than 0)");
+  if (n_wp < 1 || !waypoints) return fail(-1, "bad arguments");
+  const long long K = (n_wp - 1) * ni;
+  if (K == 0) return 0;
+  if (!q || !qd || !qdd) return fail(-1, "bad arguments");
+  int rc = h->s0.ensure((size_t)n_wp * 7);
+  rc = rc ? rc : h->s1.ensure((size_t)K * 7);
+  rc = rc ? rc : h->s2.ensure((size_t)K * 7);
+  rc = rc ? rc : h->s3.ensure((size_t)K * 7);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->s0.p, waypoints, n_wp * 7 * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  hipLaunchKernelGGL(k_minjerk, dim3(std::min<unsigned>(grid_for(K, 256), 4096)), dim3(256), 0,
+                     h->stream, h->s0.p, (long long)n_wp, (long long)ni, h->s1.p, h->s2.p, h->s3.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(q, h->s1.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(qd, h->s2.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(qdd, h->s3.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
+                       int64_t n, int32_t torque_mode, double payload_mass, int64_t* first_fail,
+                       double* tau) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || !first_fail || (n > 0 && (!q || !qd || !qdd))) return fail(-1, "bad arguments");
+  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  *first_fail = -1;
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, q, n);
+  rc = rc ? rc : upload7(h, h->s1, qd, n);
+  rc = rc ? rc : upload7(h, h->s2, qdd, n);
+  rc = rc ? rc : h->s3.ensure((size_t)n * 7);
+  rc = rc ? rc : h->u0.ensure(1);
+  if (rc) return rc;
+  HIPCHK(hipMemsetAsync(h->u0.p, 0xff, sizeof(unsigned long long), h->stream));
+  hipLaunchKernelGGL(k_validate, dim3(grid_for(n, 128)), dim3(128), 0, h->stream, h->s0.p,
+                     h->s1.p, h->s2.p, (long long)n, (int)torque_mode, payload_mass, h->u0.p,
+                     tau ? h->s3.p : nullptr);
+  HIPCHK(hipGetLastError());
+  unsigned long long ff = 0;
+  HIPCHK(hipMemcpyAsync(&ff, h->u0.p, sizeof(ff), hipMemcpyDeviceToHost, h->stream));
+  if (tau)
+    HIPCHK(hipMemcpyAsync(tau, h->s3.p, n * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *first_fail = ff == ~0ull ? -1 : (int64_t)ff;
+  return 0;
+}
+
+// ---- planner ----------------------------------------------------------------------------
+int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
+  if (int rc = set_dev(h)) return rc;
+  if (!cfg || !result) return fail(-1, "null cfg/result");
+  if (cfg->torque_mode < 0 || cfg->torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (cfg->max_nodes < 2 || cfg->max_batch < 1) return fail(-1, "bad capacities");
+  memset(result, 0, sizeof(*result));
+  result->goal_node = -1;
+  result->first_fail = -1;
+  PlanParams P = default_params();
+  for (int k = 0; k < 7; ++k) {
+    P.start[k] = cfg->start[k];
+    P.goal[k] = cfg->goal[k];
+    P.w[k] = cfg->weights[k];
+    P.res[k] = cfg->resolutions[k];
+  }
+  P.uniform_w = 1;
+  for (int k = 1; k < 7; ++k) P.uniform_w &= P.w[k] == P.w[0];
+  P.radius = cfg->radius;
+  P.goal_prob = cfg->goal_probability;
+  P.goal_tol = cfg->goal_tolerance;
+  P.mass = cfg->payload_mass;
+  P.exec_time = cfg->execution_time;
+  P.seed = cfg->seed;
+  P.torque_mode = cfg->torque_mode;
+  P.max_nodes = cfg->max_nodes;
+  h->P = P;
+  const size_t N = (size_t)cfg->max_nodes, B = (size_t)cfg->max_batch;
+  int rc = h->cfg.ensure(N * 8);
+  rc = rc ? rc : h->tgt.ensure(N * 8);
+  rc = rc ? rc : h->parent.ensure(N);
+  rc = rc ? rc : h->meta.ensure(N);
+  rc = rc ? rc : h->chain.ensure(N);
+  rc = rc ? rc : h->cand.ensure(B * 8);
+  rc = rc ? rc : h->last.ensure(B * 8);
+  rc = rc ? rc : h->cgoal.ensure(B);
+  rc = rc ? rc : h->nn.ensure(B);
+  rc = rc ? rc : h->nsafe.ensure(B);
+  rc = rc ? rc : h->nsteps.ensure(B);
+  rc = rc ? rc : h->nbr.ensure(B * kNbrCap);
+  rc = rc ? rc : h->ncount.ensure(B);
+  rc = rc ? rc : h->i0.ensure(2);
+  if (rc) return rc;
+  h->max_batch = cfg->max_batch;
+  h->samples_issued = 0;
+  h->collect_events();
+  for (double& m : h->ms) m = 0;
+  h->launches_nearest = 0;
+  // collision(start) or collision(goal) (rrt_star.py:152)
+  double sg[14];
+  memcpy(sg, cfg->start, sizeof(double) * 7);
+  memcpy(sg + 7, cfg->goal, sizeof(double) * 7);
+  int coll[2] = {0, 0};
+  if ((rc = tcmp_check_configs(h, sg, 2, coll))) return rc;
+  // root node (OptimalNode(start), rrt_star.py:155)
+  double root[8] = {0};
+  for (int k = 0; k < 7; ++k) root[k] = cfg->start[k];
+  HIPCHK(hipMemcpyAsync(h->cfg.p, root, sizeof(root), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->tgt.p, root, sizeof(root), hipMemcpyHostToDevice, h->stream));
+  int m1 = -1;
+  HIPCHK(hipMemcpyAsync(h->parent.p, &m1, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  int2 z = make_int2(0, 0);
+  HIPCHK(hipMemcpyAsync(h->meta.p, &z, sizeof(int2), hipMemcpyHostToDevice, h->stream));
+  DevState s;
+  memset(&s, 0, sizeof(s));
+  s.n_nodes = 1;
+  s.goal_node = -1;
+  s.first_fail = -1;
+  s.round_goal = INT_MAX;
+  HIPCHK(hipMemcpyAsync(h->st, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->plan_open = true;
+  result->n_nodes = 1;
+  result->status = (coll[0] || coll[1]) ? TCMP_PLAN_START_GOAL_COLLISION : TCMP_PLAN_OK;
+  if (result->status) h->plan_open = false;
+  return 0;
+}
+
+static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t* is_goal,
+                           int32_t nb) {
+  const PlanParams& P = h->P;
+  if (samples) {
+    std::vector<double> tmp((size_t)nb * 8, 0.0);
+    for (int j = 0; j < nb; ++j)
+      for (int k = 0; k < 7; ++k) tmp[8 * j + k] = samples[7 * j + k];
+    HIPCHK(hipMemcpyAsync(h->cand.p, tmp.data(), tmp.size() * sizeof(double),
+                          hipMemcpyHostToDevice, h->stream));
+    std::vector<unsigned char> g((size_t)nb, 0);
+    if (is_goal)
+      for (int j = 0; j < nb; ++j) g[j] = is_goal[j] ? 1 : 0;
+    HIPCHK(hipMemcpyAsync(h->cgoal.p, g.data(), nb, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
+  } else {
+    hipLaunchKernelGGL(k_sample, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+                       (long long)h->samples_issued, nb, h->cand.p, h->cgoal.p);
+    HIPCHK(hipGetLastError());
+  }
+  h->samples_issued += nb;
+  Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
+  hipEvent_t e0;
+  h->mark_begin(F_NEAREST, &e0);
+  const unsigned gnn = grid_for(nb, 256 * kNnCpt);
+  if (P.uniform_w)
+    hipLaunchKernelGGL(k_nearest<true>, dim3(gnn), dim3(256), 0, h->stream, P, h->st, h->cfg.p,
+                       -1LL, h->cand.p, h->cgoal.p, nb, h->nn.p, samples ? 0 : 1);
+  else
+    hipLaunchKernelGGL(k_nearest<false>, dim3(gnn), dim3(256), 0, h->stream, P, h->st, h->cfg.p,
+                       -1LL, h->cand.p, h->cgoal.p, nb, h->nn.p, samples ? 0 : 1);
+  HIPCHK(hipGetLastError());
+  h->mark_end(F_NEAREST, e0);
+  h->launches_nearest++;
+  h->mark_begin(F_EDGES, &e0);
+  EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p};
+  if (int rc = launch_edges(h, J, P)) return rc;
+  h->mark_end(F_EDGES, e0);
+  h->mark_begin(F_INSERT, &e0);
+  hipLaunchKernelGGL(k_insert, dim3(1), dim3(1024), 0, h->stream, P, h->st, tr, h->nn.p,
+                     h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb);
+  HIPCHK(hipGetLastError());
+  h->mark_end(F_INSERT, e0);
+  h->mark_begin(F_REWIRE, &e0);
+  hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+                     tr, h->nbr.p, h->ncount.p);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_rewire_apply, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+                     tr, h->nbr.p, h->ncount.p, h->scene(), h->geo());
+  HIPCHK(hipGetLastError());
+  h->mark_end(F_REWIRE, e0);
+  return 0;
+}
+
+int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
+                    int32_t* goal_found) {
+  if (int rc = set_dev(h)) return rc;
+  if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
+  if (nb < 1 || nb > h->max_batch) return fail(-1, "batch size out of range");
+  if (h->samples_issued + nb + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
+  if (int rc = plan_round_impl(h, samples, is_goal, nb)) return rc;
+  if (goal_found) {
+    long long g = -1;
+    HIPCHK(hipMemcpyAsync(&g, &h->st->goal_node, sizeof(g), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    *goal_found = g >= 0;
+  }
+  return 0;
+}
+
+int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
+  if (int rc = set_dev(h)) return rc;
+  if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
+  if (batch < 1 || batch > h->max_batch) return fail(-1, "batch size out of range");
+  if (h->samples_issued + n_samples + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
+  long long left = n_samples;
+  while (left > 0) {
+    const int nb = (int)std::min<long long>(left, batch);
+    if (int rc = plan_round_impl(h, nullptr, nullptr, nb)) return rc;
+    left -= nb;
+  }
+  return 0;
+}
+
+int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
+  if (int rc = set_dev(h)) return rc;
+  if (!r) return fail(-1, "null result");
+  if (!h->plan_open) return fail(-1, "no open plan");
+  DevState s;
+  HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  memset(r, 0, sizeof(*r));
+  r->goal_node = s.goal_node;
+  r->first_fail = -1;
+  if (s.overflow) return fail(-3, "tree capacity exceeded");
+  if (s.goal_node >= 0) {
+    // capacity for waypoints: bounded by the chain's total n_safe; allocate generously
+    const size_t wcap = std::max<size_t>(1024, (size_t)s.n_nodes * 64);
+    int rc = h->wp.ensure(std::min<size_t>(wcap, (size_t)1 << 26) * 7);
+    if (rc) return rc;
+    hipEvent_t e0;
+    h->mark_begin(F_FINISH, &e0);
+    hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->P, h->st,
+                       Tree{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p}, h->chain.p, h->wp.p,
+                       (long long)(h->wp.n / 7));
+    HIPCHK(hipGetLastError());
+    long long WK[3];
+    HIPCHK(hipMemcpyAsync(WK, &h->st->W, sizeof(WK), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    const long long K = std::max<long long>(WK[2], 1);
+    rc = h->tq.ensure(K * 7);
+    rc = rc ? rc : h->tqd.ensure(K * 7);
+    rc = rc ? rc : h->tqdd.ensure(K * 7);
+    rc = rc ? rc : h->tpsg.ensure(K);
+    rc = rc ? rc : h->ttau.ensure(K * 7);
+    if (rc) return rc;
+    hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
+    hipLaunchKernelGGL(k_traj, dim3(std::min<unsigned>(grid_for(K, 256), 2048)), dim3(256), 0,
+                       h->stream, h->P, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
+                       h->ttau.p);
+    hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
+    HIPCHK(hipGetLastError());
+    h->mark_end(F_FINISH, e0);
+    HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    if (s.status == -3) return fail(-3, "waypoint capacity exceeded");
+    r->n_waypoints = s.W;
+    r->n_traj = s.status == TCMP_PLAN_MINJERK_ASSERT ? 0 : s.K;
+    r->first_fail = s.first_fail;
+    r->status = s.status;
+    r->goal_found = 1;
+  } else {
+    HIPCHK(hipStreamSynchronize(h->stream));
+    r->status = TCMP_PLAN_NO_GOAL;
+  }
+  h->collect_events();
+  r->n_nodes = s.n_nodes;
+  r->n_samples = s.samples;
+  r->edge_steps = s.edge_steps;
+  r->pairs_tested = s.pairs_tested;
+  r->pairs_sat = s.pairs_sat;
+  r->pairs_exact = s.pairs_exact;
+  r->nn_pairs = s.nn_pairs;
+  r->ms_nearest = h->ms[F_NEAREST];
+  r->ms_edges = h->ms[F_EDGES];
+  r->ms_insert = h->ms[F_INSERT];
+  r->ms_rewire = h->ms[F_REWIRE];
+  r->ms_finish = h->ms[F_FINISH];
+  r->launches_nearest = h->launches_nearest;
+  return 0;
+}
+
+int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
+                    double* psg, double* tau) {
+  if (int rc = set_dev(h)) return rc;
+  DevState s;
+  HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  if (s.goal_node < 0) return fail(-1, "no plan to fetch");
+  const long long W = s.W, K = s.status == TCMP_PLAN_MINJERK_ASSERT ? 0 : s.K;
+  if (waypoints && W)
+    HIPCHK(hipMemcpyAsync(waypoints, h->wp.p, W * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (K) {
+    if (q) HIPCHK(hipMemcpyAsync(q, h->tq.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (qd) HIPCHK(hipMemcpyAsync(qd, h->tqd.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (qdd) HIPCHK(hipMemcpyAsync(qdd, h->tqdd.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (psg) HIPCHK(hipMemcpyAsync(psg, h->tpsg.p, K * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+    if (tau) HIPCHK(hipMemcpyAsync(tau, h->ttau.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  }
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32_t* parent,
+                   int64_t* n) {
+  if (int rc = set_dev(h)) return rc;
+  if (!n) return fail(-1, "null n");
+  long long nn = 0;
+  HIPCHK(hipMemcpyAsync(&nn, &h->st->n_nodes, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *n = nn;
+  const long long m = std::min<long long>(nn, cap);
+  if (m <= 0) return 0;
+  std::vector<double> tmp((size_t)m * 8);
+  HIPCHK(hipMemcpyAsync(tmp.data(), h->cfg.p, tmp.size() * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  if (parent)
+    HIPCHK(hipMemcpyAsync(parent, h->parent.p, m * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (long long i = 0; i < m; ++i) {
+    if (cfg)
+      for (int k = 0; k < 7; ++k) cfg[7 * i + k] = tmp[8 * i + k];
+    if (cost) cost[i] = tmp[8 * i + 7];
+  }
+  return 0;
+}
+
+}  // extern "C"

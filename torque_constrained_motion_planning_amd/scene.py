@@ -1,0 +1,132 @@
+"""Scene records that replace the reference's pybullet body handles.
+
+The reference passes pybullet body ids around (`Problem.robot`, `Problem.fixed`,
+`Problem.payload`, utils.py:86-93) and asks Bullet for link poses and closest points.  The
+engine needs only geometry, so bodies become plain records:
+
+  PandaRobot  -- the Panda of src/models/panda_mod.urdf (joint limits, efforts, fingers open)
+  Box         -- a fixed oriented box obstacle (URDF <box> collision, e.g. table_wooden.urdf)
+  Payload     -- the grasped object (mass for the torque tests, cylinder/box for grasps)
+
+`obstacle_array()` packs obstacles into the C-ABI layout (15 doubles per box).
+"""
+import numpy as np
+
+# panda_mod.urdf:121-285
+JOINT_LOWER = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+JOINT_UPPER = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+JOINT_EFFORT = np.array([87.0, 87.0, 87.0, 87.0, 12.0, 12.0, 12.0])
+JOINT_VELOCITY = np.array([2.175, 2.175, 2.175, 2.175, 2.61, 2.61, 2.61])
+ARM_JOINT_NAMES = ['panda_joint1', 'panda_joint2', 'panda_joint3', 'panda_joint4',
+                   'panda_joint5', 'panda_joint6', 'panda_joint7']  # utils.py:29-30
+COLLISION_LINK_NAMES = ['panda_link1', 'panda_link2', 'panda_link3', 'panda_link4',
+                        'panda_link5', 'panda_link6', 'panda_link7', 'panda_hand',
+                        'panda_leftfinger', 'panda_rightfinger']
+
+
+class PandaRobot:
+    """The planning robot (replaces the pybullet body id of panda_mod.urdf).
+
+    Base frame = world frame; fingers held open at 0.04 (open_arm, panda_primitives.py:320).
+    """
+    name = "panda"
+
+    def __init__(self):
+        self.joints = list(range(7))
+        self.lower = JOINT_LOWER.copy()
+        self.upper = JOINT_UPPER.copy()
+        self.effort = JOINT_EFFORT.copy()
+        self.velocity = JOINT_VELOCITY.copy()
+        self.conf = None
+
+    def __repr__(self):
+        return "PandaRobot()"
+
+
+def rotation_rpy(roll=0.0, pitch=0.0, yaw=0.0):
+    cr, sr = np.cos(roll), np.sin(roll)
+    cp, sp = np.cos(pitch), np.sin(pitch)
+    cy, sy = np.cos(yaw), np.sin(yaw)
+    Rx = np.array([[1, 0, 0], [0, cr, -sr], [0, sr, cr]])
+    Ry = np.array([[cp, 0, sp], [0, 1, 0], [-sp, 0, cp]])
+    Rz = np.array([[cy, -sy, 0], [sy, cy, 0], [0, 0, 1]])
+    return Rz @ Ry @ Rx
+
+
+class Box:
+    """Fixed oriented box obstacle: centre, full size (URDF <box size>), rotation."""
+
+    def __init__(self, center, size=None, half_extents=None, rotation=None, name="box"):
+        self.center = np.asarray(center, dtype=np.float64).reshape(3)
+        if half_extents is None:
+            half_extents = np.asarray(size, dtype=np.float64).reshape(3) / 2.0
+        self.half_extents = np.asarray(half_extents, dtype=np.float64).reshape(3)
+        self.rotation = np.eye(3) if rotation is None else np.asarray(rotation, dtype=np.float64).reshape(3, 3)
+        self.name = name
+
+    def obb15(self):
+        return np.concatenate([self.center, self.rotation.reshape(-1), self.half_extents])
+
+    def __repr__(self):
+        return "Box(%s, half=%s)" % (np.round(self.center, 4).tolist(), np.round(self.half_extents, 4).tolist())
+
+
+class Payload:
+    """Grasped object: mass (get_mass) and a cylinder/box shape for top grasps."""
+
+    def __init__(self, mass, radius=0.015, height=0.05, pose=None, name="payload"):
+        self.mass = float(mass)
+        self.radius = float(radius)
+        self.height = float(height)
+        self.pose = pose
+        self.name = name
+
+
+def get_mass(body):
+    """utils.get_mass replacement (pybullet getDynamicsInfo mass)."""
+    return float(getattr(body, "mass", 0.0))
+
+
+def obstacle_array(fixed):
+    """Pack Problem.fixed into the (n, 15) C-ABI layout."""
+    if fixed is None:
+        fixed = []
+    if isinstance(fixed, np.ndarray):
+        if fixed.size == 0:
+            return np.zeros((0, 15))
+        return np.ascontiguousarray(fixed.astype(np.float64).reshape(-1, 15))
+    rows = []
+    for b in fixed:
+        if isinstance(b, Box):
+            rows.append(b.obb15())
+        else:
+            a = np.asarray(b, dtype=np.float64).reshape(-1)
+            if a.size != 15:
+                raise TypeError("obstacles must be Box records or 15-vectors (centre, R, half)")
+            rows.append(a)
+    if not rows:
+        return np.zeros((0, 15))
+    return np.ascontiguousarray(np.array(rows, dtype=np.float64))
+
+
+def random_box_scene(rng, n, avoid=(), collides=None, aligned=True, max_tries=100000):
+    """SURVEY 8d synthetic scene: centres U([0.2,0.8]x[-0.6,0.6]x[0,0.8]) m, half extents
+    U[0.03,0.12] m, rejected while any configuration in `avoid` collides (collides(q, obs))."""
+    boxes = []
+    tries = 0
+    while len(boxes) < n:
+        tries += 1
+        if tries > max_tries:
+            raise RuntimeError("could not place %d boxes" % n)
+        c = rng.uniform([0.2, -0.6, 0.0], [0.8, 0.6, 0.8])
+        h = rng.uniform(0.03, 0.12, 3)
+        R = np.eye(3)
+        if not aligned:
+            R = rotation_rpy(*rng.uniform(-np.pi, np.pi, 3))
+        b = Box(c, half_extents=h, rotation=R)
+        if collides is not None and avoid:
+            arr = obstacle_array([b])
+            if any(collides(q, arr) for q in avoid):
+                continue
+        boxes.append(b)
+    return boxes
