@@ -43,7 +43,8 @@ int fail(int code, const std::string& msg) {
       return fail(-2, std::string(#x) + ": " + hipGetErrorString(e_));                 \
   } while (0)
 
-constexpr int kNbrCap = 8;     // stored rewire neighbours per new node
+constexpr int kNbrCap = 8;     // stored rewire neighbours per flagged new node
+constexpr int kMaxSplits = 64; // tree splits of k_nearest
 constexpr int kNnTile = 256;   // tree nodes per LDS tile
 constexpr int kNnCpt = 2;      // candidates per thread in k_nearest
 
@@ -57,6 +58,7 @@ struct DevState {
   unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
   int work_counter;
   int round_goal;
+  int rw_count;
   int status;
   int overflow;
 };
@@ -114,33 +116,46 @@ __global__ void k_sample(PlanParams P, DevState* st, long long base, int nb, dou
 }
 
 // ------------------------------------------------------------------------------------------
-// k_nearest: argmin_n sum_k w_k (s_k - n_k)^2 over the snapshot, ties -> lowest index.
-// Block = 256 threads x kNnCpt candidates; the tree streams through LDS in 256-node tiles
-// (16 KiB) that every lane reads by broadcast.
+// k_goal_fix: the round's goal-biased lane takes the goal configuration (rrt_star.py:160-161)
+// ------------------------------------------------------------------------------------------
+__global__ void k_goal_fix(PlanParams P, DevState* st, double* cand, unsigned char* cgoal, int nb) {
+  const int j = st->round_goal;
+  if (threadIdx.x == 0 && j < nb) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = P.goal[k];
+    cgoal[j] = 1;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_nearest: argmin_n sum_k w_k (s_k - n_k)^2 over the snapshot, ties -> lowest index
+// (rrt_star.py:9-14,171).  grid = (candidate blocks, tree splits): block (x, y) scores
+// 256 x kNnCpt candidates against nodes [y*split_len, (y+1)*split_len); the nodes stream
+// through LDS in 256-node tiles (16 KiB) read by broadcast.  Each candidate also tracks its
+// second-smallest distance: k_nn_merge uses it to prove that no node other than the nearest
+// can lie within the rewire radius of the new node (triangle inequality), so the full
+// neighbour scan of rrt_star.py:183 runs only for the rare lanes where that proof fails.
 // ------------------------------------------------------------------------------------------
 template <bool UW>
 __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, const double* tree,
-                                                 long long T_override, double* cand,
-                                                 unsigned char* cgoal, int nb, int* nn,
-                                                 int device_sampled) {
+                                                 long long T_override, const double* cand,
+                                                 int nb, long long split_len, double* pd1,
+                                                 int* pidx, double* pd2) {
   __shared__ double4 tile[2 * kNnTile];
   const int tid = threadIdx.x;
   const long long T = T_override >= 0 ? T_override : st->n_nodes;
-  const int rg = device_sampled ? st->round_goal : INT_MAX;
+  const long long lo = (long long)blockIdx.y * split_len;
+  const long long hi = min(T, lo + split_len);
   double s[kNnCpt][7];
-  double best[kNnCpt];
+  double b1[kNnCpt], b2[kNnCpt];
   int bi[kNnCpt];
 #pragma unroll
   for (int c = 0; c < kNnCpt; ++c) {
     const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
-    best[c] = INFINITY;
-    bi[c] = 0;
+    b1[c] = INFINITY;
+    b2[c] = INFINITY;
+    bi[c] = INT_MAX;
     if (j < nb) {
-      if (j == rg) {  // the round's goal-biased lane (rrt_star.py:160-161)
-#pragma unroll
-        for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = P.goal[k];
-        cgoal[j] = 1;
-      }
       load7(cand + 8 * (size_t)j, s[c]);
     } else {
 #pragma unroll
@@ -151,14 +166,14 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
 #pragma unroll
   for (int k = 0; k < 7; ++k) w[k] = P.w[k];
   const double4* t4 = reinterpret_cast<const double4*>(tree);
-  for (long long base = 0; base < T; base += kNnTile) {
+  for (long long base = lo; base < hi; base += kNnTile) {
     const long long n = base + tid;
-    if (n < T) {
+    if (n < hi) {
       tile[2 * tid] = t4[2 * n];
       tile[2 * tid + 1] = t4[2 * n + 1];
     }
     __syncthreads();
-    const int cnt = (int)min((long long)kNnTile, T - base);
+    const int cnt = (int)min((long long)kNnTile, hi - base);
     for (int jj = 0; jj < cnt; ++jj) {
       const double4 a = tile[2 * jj], b = tile[2 * jj + 1];
 #pragma unroll
@@ -176,10 +191,11 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
           dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
           dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
         }
-        if (dd < best[c]) {
-          best[c] = dd;
-          bi[c] = (int)(base + jj);
-        }
+        // top-2 (strict <: the first index keeps ties, rrt_star.py:14)
+        const bool lt1 = dd < b1[c];
+        b2[c] = lt1 ? b1[c] : fmin(b2[c], dd);
+        b1[c] = lt1 ? dd : b1[c];
+        bi[c] = lt1 ? (int)(base + jj) : bi[c];
       }
     }
     __syncthreads();
@@ -187,9 +203,39 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
 #pragma unroll
   for (int c = 0; c < kNnCpt; ++c) {
     const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
-    if (j < nb) nn[j] = bi[c];
+    if (j < nb) {
+      const size_t o = (size_t)blockIdx.y * nb + j;
+      pd1[o] = b1[c];
+      pidx[o] = bi[c];
+      pd2[o] = b2[c];
+    }
   }
-  if (blockIdx.x == 0 && tid == 0) atomicAdd(&st->nn_pairs, (unsigned long long)nb * (unsigned long long)T);
+  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
+    atomicAdd(&st->nn_pairs, (unsigned long long)nb * (unsigned long long)T);
+}
+
+// merge the per-split partial results: nearest index and the second-smallest distance
+template <bool UW>
+__global__ void k_nn_merge(int nb, int splits, const double* pd1, const int* pidx,
+                           const double* pd2, int* nn, double* second) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  double b1 = INFINITY, b2 = INFINITY;
+  int bi = INT_MAX;
+  for (int y = 0; y < splits; ++y) {
+    const size_t o = (size_t)y * nb + j;
+    const double d1 = pd1[o], d2 = pd2[o];
+    const int i1 = pidx[o];
+    if (d1 < b1 || (d1 == b1 && i1 < bi)) {
+      b2 = fmin(b1, d2);
+      b1 = d1;
+      bi = i1;
+    } else {
+      b2 = fmin(b2, d1);
+    }
+  }
+  nn[j] = bi == INT_MAX ? 0 : bi;
+  if (second) second[j] = b2;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -289,7 +335,8 @@ __global__ __launch_bounds__(256) void k_edges(EdgeJob J, PlanParams P, Scene sc
 __global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tree tr,
                                                  const int* nn, const double* cand,
                                                  const unsigned char* cgoal, const int* nsafe,
-                                                 const int* nsteps, const double* last, int nb) {
+                                                 const int* nsteps, const double* last, int nb,
+                                                 const double* second, int* rwlist) {
   __shared__ int scan[1024];
   __shared__ long long gbest[1024];
   const int tid = threadIdx.x;
@@ -297,6 +344,7 @@ __global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tre
   const bool goal_open = st->goal_node < 0;
   const int chunk = (nb + 1023) / 1024;
   const int j0 = min(nb, tid * chunk), j1 = min(nb, j0 + chunk);
+  if (tid == 0) st->rw_count = 0;
   int cnt = 0;
   for (int j = j0; j < j1; ++j) cnt += nsafe[j] > 0;
   scan[tid] = cnt;
@@ -327,6 +375,21 @@ __global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tre
       store7(tr.tgt + 8 * idx, tq);
       tr.meta[idx] = make_int2(nsteps[j], nsafe[j]);
       if (goal_open && cgoal[j] && distance(lq, P.goal, P.w) < P.goal_tol) best = min(best, idx);
+      {
+        // Rewire neighbours n != nearest of the new node satisfy, by the triangle inequality,
+        // d(n, s) <= d(n, new) + d(new, s) < radius + d(new, s); the nearest itself never
+        // rewires (equal cost).  Only lanes whose second-nearest node passes that bound get
+        // the neighbour scan.  Distances in the metric k_nearest used (unweighted if UW).
+        double e2 = 0;
+#pragma unroll
+        for (int k = 0; k < 7; ++k) {
+          const double d = lq[k] - tq[k];
+          e2 = fma(P.uniform_w ? d : P.w[k] * d, d, e2);
+        }
+        const double r = P.uniform_w ? P.radius / sqrt(P.w[0]) : P.radius;
+        const double t = sqrt(e2) + r;
+        if (second[j] < t * t * (1.0 + 1e-9) + 1e-300) rwlist[atomicAdd(&st->rw_count, 1)] = (int)idx;
+      }
       ++idx;
     }
   }
@@ -356,15 +419,17 @@ __global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tre
 // round's snapshot, visited in index order; reparent when cheaper and the edge is safe.
 // ------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st, Tree tr,
-                                                     int* nbr, int* ncount) {
+                                                     const int* rwlist, int* nbr, int* ncount) {
+  // neighbours within `radius` of each flagged new node among the snapshot, in index order
+  // (the order rrt_star.py:187 visits them); the snapshot streams through LDS tiles
   __shared__ double4 tile[2 * kNnTile];
   const int tid = threadIdx.x;
-  const long long A = st->new_count, T = st->snap;
-  if ((long long)blockIdx.x * 256 >= A) return;  // block-uniform
+  const long long R = st->rw_count, T = st->snap;
+  if ((long long)blockIdx.x * 256 >= R) return;  // block-uniform
   const long long t = (long long)blockIdx.x * 256 + tid;
-  const bool act = t < A;
+  const bool act = t < R;
   double qn[7];
-  if (act) load7(tr.cfg + 8 * (T + t), qn);
+  if (act) load7(tr.cfg + 8 * (long long)rwlist[t], qn);
   else for (int k = 0; k < 7; ++k) qn[k] = 1e30;
   const double r2 = P.radius * P.radius;
   int c = 0;
@@ -398,13 +463,13 @@ __global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st,
 }
 
 __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st, Tree tr,
-                                                      const int* nbr, const int* ncount,
-                                                      Scene sc, Geo g) {
-  const long long A = st->new_count, T = st->snap;
+                                                      const int* rwlist, const int* nbr,
+                                                      const int* ncount, Scene sc, Geo g) {
+  const long long R = st->rw_count, T = st->snap;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const bool act = t < A && ncount[t] > 0;
+  const bool act = t < R && ncount[t] > 0;
   if (__ballot(act) == 0) return;  // wave-uniform
-  const long long me = T + t;
+  const long long me = act ? rwlist[t] : 0;
   double qn[7];
   double cost_new = 0;
   int cnt = 0;
@@ -774,7 +839,9 @@ struct tcmp_handle {
   DBuf<int2> meta;
   DBuf<double> cand, last;
   DBuf<unsigned char> cgoal;
-  DBuf<int> nn, nsafe, nsteps, nbr, ncount;
+  DBuf<int> nn, nsafe, nsteps, nbr, ncount, pidx, rwlist;
+  DBuf<double> pd1, pd2;
+  DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
   long long samples_issued = 0;
@@ -845,6 +912,33 @@ int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
 }
 
 unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>(1, (n + block - 1) / block); }
+
+// k_nearest over a tree of at most T_bound nodes (T_exact >= 0: known size), then merge.
+int launch_nearest(tcmp_handle* h, const PlanParams& P, const double* tree, long long T_bound,
+                   long long T_exact, const double* cand, int nb, int* nn, double* second) {
+  const int cblocks = (nb + 256 * kNnCpt - 1) / (256 * kNnCpt);
+  const long long want = std::max<long long>(1, (8LL * h->cu_count + cblocks - 1) / cblocks);
+  long long splits = std::min<long long>(want, std::max<long long>(1, T_bound / 2048));
+  splits = std::min<long long>(splits, kMaxSplits);
+  long long len = (T_bound + splits - 1) / splits;
+  len = ((len + kNnTile - 1) / kNnTile) * kNnTile;
+  splits = std::max<long long>(1, (T_bound + len - 1) / len);
+  if (int rc = h->pd1.ensure((size_t)splits * nb)) return rc;
+  if (int rc = h->pd2.ensure((size_t)splits * nb)) return rc;
+  if (int rc = h->pidx.ensure((size_t)splits * nb)) return rc;
+  const dim3 grid((unsigned)cblocks, (unsigned)splits);
+  if (P.uniform_w)
+    hipLaunchKernelGGL(k_nearest<true>, grid, dim3(256), 0, h->stream, P, h->st, tree, T_exact,
+                       cand, nb, len, h->pd1.p, h->pidx.p, h->pd2.p);
+  else
+    hipLaunchKernelGGL(k_nearest<false>, grid, dim3(256), 0, h->stream, P, h->st, tree, T_exact,
+                       cand, nb, len, h->pd1.p, h->pidx.p, h->pd2.p);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_nn_merge<true>, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, nb,
+                     (int)splits, h->pd1.p, h->pidx.p, h->pd2.p, nn, second);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
 
 int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   if (J.n <= 0) return 0;
@@ -927,10 +1021,13 @@ int tcmp_destroy(tcmp_handle* h) {
                   &h->s1, &h->s2, &h->s3})
     b->release();
   for (auto* b : {&h->parent, &h->nn, &h->nsafe, &h->nsteps, &h->nbr, &h->ncount, &h->i0,
-                  &h->i1, &h->i2})
+                  &h->i1, &h->i2, &h->pidx, &h->rwlist})
     b->release();
+  h->pd1.release();
+  h->pd2.release();
   h->meta.release();
   h->cgoal.release();
+  h->second.release();
   h->chain.release();
   h->u0.release();
   for (auto& p : h->ev_used) {
@@ -1073,14 +1170,8 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
       uw &= weights[k] == weights[0];
     }
   }
-  const unsigned grid = grid_for(n, 256 * kNnCpt);
-  if (uw)
-    hipLaunchKernelGGL(k_nearest<true>, dim3(grid), dim3(256), 0, h->stream, P, h->st, h->s0.p,
-                       (long long)T, h->s1.p, h->cgoal.p, (int)n, h->i0.p, 0);
-  else
-    hipLaunchKernelGGL(k_nearest<false>, dim3(grid), dim3(256), 0, h->stream, P, h->st, h->s0.p,
-                       (long long)T, h->s1.p, h->cgoal.p, (int)n, h->i0.p, 0);
-  HIPCHK(hipGetLastError());
+  P.uniform_w = uw ? 1 : 0;
+  if ((rc = launch_nearest(h, P, h->s0.p, T, T, h->s1.p, (int)n, h->i0.p, nullptr))) return rc;
   HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1180,6 +1271,8 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->nsteps.ensure(B);
   rc = rc ? rc : h->nbr.ensure(B * kNbrCap);
   rc = rc ? rc : h->ncount.ensure(B);
+  rc = rc ? rc : h->second.ensure(B);
+  rc = rc ? rc : h->rwlist.ensure(B);
   rc = rc ? rc : h->i0.ensure(2);
   if (rc) return rc;
   h->max_batch = cfg->max_batch;
@@ -1240,14 +1333,15 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
   hipEvent_t e0;
   h->mark_begin(F_NEAREST, &e0);
-  const unsigned gnn = grid_for(nb, 256 * kNnCpt);
-  if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest<true>, dim3(gnn), dim3(256), 0, h->stream, P, h->st, h->cfg.p,
-                       -1LL, h->cand.p, h->cgoal.p, nb, h->nn.p, samples ? 0 : 1);
-  else
-    hipLaunchKernelGGL(k_nearest<false>, dim3(gnn), dim3(256), 0, h->stream, P, h->st, h->cfg.p,
-                       -1LL, h->cand.p, h->cgoal.p, nb, h->nn.p, samples ? 0 : 1);
-  HIPCHK(hipGetLastError());
+  if (!samples) {
+    hipLaunchKernelGGL(k_goal_fix, dim3(1), dim3(64), 0, h->stream, P, h->st, h->cand.p,
+                       h->cgoal.p, nb);
+    HIPCHK(hipGetLastError());
+  }
+  // the snapshot holds at most 1 + (samples issued before this round) nodes
+  if (int rc = launch_nearest(h, P, h->cfg.p, 1 + h->samples_issued - nb, -1, h->cand.p, nb,
+                              h->nn.p, h->second.p))
+    return rc;
   h->mark_end(F_NEAREST, e0);
   h->launches_nearest++;
   h->mark_begin(F_EDGES, &e0);
@@ -1256,15 +1350,16 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   h->mark_end(F_EDGES, e0);
   h->mark_begin(F_INSERT, &e0);
   hipLaunchKernelGGL(k_insert, dim3(1), dim3(1024), 0, h->stream, P, h->st, tr, h->nn.p,
-                     h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb);
+                     h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->second.p,
+                     h->rwlist.p);
   HIPCHK(hipGetLastError());
   h->mark_end(F_INSERT, e0);
   h->mark_begin(F_REWIRE, &e0);
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
-                     tr, h->nbr.p, h->ncount.p);
+                     tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_rewire_apply, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
-                     tr, h->nbr.p, h->ncount.p, h->scene(), h->geo());
+                     tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);
   return 0;
@@ -1310,7 +1405,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   memset(r, 0, sizeof(*r));
   r->goal_node = s.goal_node;
   r->first_fail = -1;
-  if (s.overflow) return fail(-3, "tree capacity exceeded");
+  if (s.overflow == 1) return fail(-3, "tree capacity exceeded");
   if (s.goal_node >= 0) {
     // capacity for waypoints: bounded by the chain's total n_safe; allocate generously
     const size_t wcap = std::max<size_t>(1024, (size_t)s.n_nodes * 64);
