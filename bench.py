@@ -25,7 +25,7 @@ import numpy as np
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from torque_constrained_motion_planning_amd import _lib  # noqa: E402
+from torque_constrained_motion_planning_amd import _lib, shard  # noqa: E402
 from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene  # noqa: E402
 
 START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])  # utils.py:45
@@ -98,7 +98,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--samples", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=131072)
+    ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--obstacles", type=int, default=16)
     ap.add_argument("--cpu-samples", type=int, default=20000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -126,34 +126,24 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    def gather(out):
+    def gather(out, qid):
         # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
         if dist is None:
             return
-        import torch
-        K = 0 if out is None else len(out["q"])
-        n = torch.tensor([K], device="cuda", dtype=torch.int64)
-        ns = [torch.zeros_like(n) for _ in range(world)]
-        dist.all_gather(ns, n)
-        kmax = max(int(x.item()) for x in ns)
-        buf = torch.zeros((max(kmax, 1), 22), device="cuda", dtype=torch.float64)
-        if K:
-            buf[:K] = torch.from_numpy(np.concatenate(
-                [out["q"], out["qd"], out["qdd"], out["psg"][:, None]], axis=1)).cuda()
-        outs = [torch.zeros_like(buf) for _ in range(world)] if rank == 0 else None
-        dist.gather(buf, outs, dst=0)
+        shard.gather_trajectories(dist, [shard.pack_trajectory(out)], [qid], world, rank,
+                                  device="cuda")
 
     step_seed = lambda s: 1234 + rank * 100003 + s  # noqa: E731
     for w in range(args.warmup):
         r, out = run_query(eng, obs, goal, args.samples, args.batch, step_seed(10_000 + w))
-        gather(out)
+        gather(out, w)
 
     barrier()
     t0 = time.perf_counter()
     results = []
     for s in range(args.steps):
         r, out = run_query(eng, obs, goal, args.samples, args.batch, step_seed(s))
-        gather(out)
+        gather(out, s * world + rank)
         results.append(r.as_dict())
     barrier()
     dt = time.perf_counter() - t0
@@ -169,10 +159,17 @@ def main():
     nn_ms = sum(x["ms_nearest"] for x in results)
     nn_launches = sum(x["launches_nearest"] for x in results)
     achieved_tflops = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    # algorithmic HBM bytes: each block streams the tree snapshot once
-    nn_blocks_bytes = 0.0
-    for x in results:
-        pass
+    # HBM traffic per k_nearest launch from the committed rocprofv3 PMC passes of this same
+    # workload (profiles/*_pmc_hbm.json; FETCH_SIZE doubled per the gfx950 correction)
+    traffic = None
+    pmc = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_hbm.json")) \
+        if os.path.isdir(os.path.join(REPO, "profiles")) else []
+    if pmc:
+        d = json.load(open(os.path.join(REPO, "profiles", pmc[-1])))["dispatches"].get("k_nearest", [])
+        fetch = [x["value_KiB"] for x in d if x["counter"] == "FETCH_SIZE"]
+        write = [x["value_KiB"] for x in d if x["counter"] == "WRITE_SIZE"]
+        if fetch and len(fetch) == len(write):
+            traffic = (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
     kernel_ms = {k: sum(x[k] for x in results) / args.steps for k in
                  ("ms_nearest", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
     if args.verbose and rank == 0:
@@ -203,7 +200,8 @@ def main():
             "peak": PEAK_FP64_TFLOPS,
             "unit": "TFLOP/s",
             "frac": achieved_tflops / PEAK_FP64_TFLOPS,
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes per launch (rocprofv3 PMC, %s)" % (pmc[-1] if pmc else "none"),
             "algorithmic": "%d flop per (candidate, node) pair; %d pairs over %d launches" % (
                 NN_FLOP_PER_PAIR, nn_pairs, nn_launches),
         },
