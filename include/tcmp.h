@@ -119,6 +119,7 @@ typedef struct {
   double ms_rewire;
   double ms_finish;
   int64_t launches_nearest;
+  uint64_t nn_box_tests;  /* (candidate, chunk-box) lower-bound tests of the pruned scan */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

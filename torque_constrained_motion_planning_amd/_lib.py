@@ -54,6 +54,7 @@ class PlanResult(ctypes.Structure):
         ("ms_nearest", ctypes.c_double), ("ms_edges", ctypes.c_double),
         ("ms_insert", ctypes.c_double), ("ms_rewire", ctypes.c_double),
         ("ms_finish", ctypes.c_double), ("launches_nearest", ctypes.c_int64),
+        ("nn_box_tests", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -14,10 +14,12 @@
 //   k_rewire_apply  sequential rewire per new node (rrt_star.py:187-192)
 // then k_retrace / k_traj (min-jerk + final dynamic torque validation).
 #include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <climits>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -56,6 +58,7 @@ struct DevState {
   long long samples;
   long long W, ni, K, first_fail;
   unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
+  unsigned long long nn_box_tests;
   int work_counter;
   int round_goal;
   int rw_count;
@@ -213,6 +216,205 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
   if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
     atomicAdd(&st->nn_pairs, (unsigned long long)nb * (unsigned long long)T);
 }
+
+// ------------------------------------------------------------------------------------------
+// Morton-chunked exact nearest neighbour.
+// Each round the snapshot is sorted by a 63-bit Morton key (9 bits per joint over the joint
+// limits), cut into 256-node chunks with axis-aligned bounds, and every wave scores 128
+// Morton-sorted candidates against the chunks in zig-zag order from the candidates' own
+// position, skipping a chunk when the box lower bound exceeds every lane's current best
+// (plus the rewire radius, so the second-nearest stays exact within the range k_insert's
+// rewire bound needs).  Ties compare (distance, original index): the first index wins as in
+// rrt_star.py:14, whatever the visiting order.
+// ------------------------------------------------------------------------------------------
+constexpr int kChunk = 256;
+
+__device__ __forceinline__ unsigned long long morton7(const double q[7]) {
+  unsigned u[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    double t = (q[k] - kLo[k]) / (kHi[k] - kLo[k]);
+    t = fmin(fmax(t, 0.0), 1.0);
+    u[k] = (unsigned)(t * 511.0);
+  }
+  unsigned long long key = 0;
+#pragma unroll
+  for (int b = 8; b >= 0; --b)
+#pragma unroll
+    for (int k = 0; k < 7; ++k) key = (key << 1) | ((u[k] >> b) & 1u);
+  return key;
+}
+
+__global__ void k_node_keys(DevState* st, const double* cfg, long long T_bound,
+                            unsigned long long* keys, int* vals) {
+  const long long T = st->n_nodes;
+  for (long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x; n < T_bound;
+       n += (long long)gridDim.x * blockDim.x) {
+    unsigned long long key = ~0ull;
+    if (n < T) {
+      double q[7];
+      load7(cfg + 8 * n, q);
+      key = morton7(q);
+    }
+    keys[n] = key;
+    vals[n] = (int)n;
+  }
+}
+
+__global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys, int* vals) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= nb) return;
+  double q[7];
+  load7(cand + 8 * (size_t)j, q);
+  keys[j] = morton7(q);
+  vals[j] = j;
+}
+
+#if 0  // first chunked scan (128 candidates per wave), superseded by tcmp_nn.h
+// sorted snapshot: stree[p] = (q0..q6, original index); cbox[c] = (lo0..6, -, hi0..6, -)
+__global__ __launch_bounds__(256) void k_build_chunks(DevState* st, const double* cfg,
+                                                      const int* svals, double* stree,
+                                                      double* cbox) {
+  __shared__ double red[2][7][4];
+  const long long T = st->n_nodes;
+  const long long p = (long long)blockIdx.x * kChunk + threadIdx.x;
+  if ((long long)blockIdx.x * kChunk >= T) return;  // block-uniform
+  double q[7];
+  double lo[7], hi[7];
+  if (p < T) {
+    const int n = svals[p];
+    load7(cfg + 8 * (size_t)n, q);
+    store7(stree + 8 * p, q);
+    stree[8 * p + 7] = (double)n;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lo[k] = q[k]; hi[k] = q[k]; }
+  } else {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    lo[k] = wave_min(lo[k]);
+    hi[k] = wave_max(hi[k]);
+  }
+  const int w = threadIdx.x >> 6;
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) { red[0][k][w] = lo[k]; red[1][k][w] = hi[k]; }
+  }
+  __syncthreads();
+  if (threadIdx.x < 7) {
+    const int k = threadIdx.x;
+    double a = red[0][k][0], b = red[1][k][0];
+    for (int i = 1; i < 4; ++i) { a = fmin(a, red[0][k][i]); b = fmax(b, red[1][k][i]); }
+    cbox[16 * (size_t)blockIdx.x + k] = a;
+    cbox[16 * (size_t)blockIdx.x + 8 + k] = b;
+  }
+}
+
+template <bool UW>
+__device__ __forceinline__ void nn_update(const double s[7], const double* nd, double w[7],
+                                          double& b1, double& b2, int& bi, double& thr, double ru) {
+  const double d0 = s[0] - nd[0], d1 = s[1] - nd[1], d2 = s[2] - nd[2], d3 = s[3] - nd[3],
+               d4 = s[4] - nd[4], d5 = s[5] - nd[5], d6 = s[6] - nd[6];
+  double dd;
+  if (UW) {
+    dd = d0 * d0;
+    dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
+    dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
+  } else {
+    dd = w[0] * (d0 * d0);
+    dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
+    dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
+  }
+  if (dd <= b1) {
+    const int idx = (int)nd[7];
+    if (dd < b1 || idx < bi) {
+      b2 = b1;
+      b1 = dd;
+      bi = idx;
+      const double t = sqrt(b1) + ru;
+      thr = t * t * (1.0 + 1e-9) + 1e-300;
+    } else {
+      b2 = fmin(b2, dd);
+    }
+  } else {
+    b2 = fmin(b2, dd);
+  }
+}
+
+template <bool UW>
+__global__ __launch_bounds__(256) void k_nearest_chunked(PlanParams P, DevState* st,
+                                                         const double* stree, const double* cbox,
+                                                         const unsigned long long* skeys,
+                                                         const double* cand, const int* cperm,
+                                                         const unsigned long long* ckeys,
+                                                         int nb, int* nn, double* second) {
+  const int lane = lane_id();
+  const int wave = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
+  const int base = wave * 128;
+  if (base >= nb) return;  // wave-uniform
+  const long long T = st->n_nodes;
+  const int nc = (int)((T + kChunk - 1) / kChunk);
+  const int j0 = base + lane, j1 = base + 64 + lane;
+  const bool a0 = j0 < nb, a1 = j1 < nb;
+  const int l0 = a0 ? cperm[j0] : 0, l1 = a1 ? cperm[j1] : 0;
+  double s0[7], s1[7];
+  load7(cand + 8 * (size_t)l0, s0);
+  load7(cand + 8 * (size_t)l1, s1);
+  double w[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) w[k] = P.w[k];
+  const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
+  double b10 = INFINITY, b20 = INFINITY, thr0 = INFINITY;
+  double b11 = INFINITY, b21 = INFINITY, thr1 = INFINITY;
+  int bi0 = INT_MAX, bi1 = INT_MAX;
+  // home chunk of the wave: position of its first candidate's key in the sorted snapshot
+  const unsigned long long hk = ckeys[base];
+  long long lo = 0, hi = T;
+  while (lo < hi) {
+    const long long mid = (lo + hi) >> 1;
+    if (skeys[mid] < hk) lo = mid + 1; else hi = mid;
+  }
+  const int c0 = (int)min((long long)nc - 1, lo / kChunk);
+  int up = c0, dn = c0 - 1;
+  bool turn_up = true;
+  unsigned long long scanned = 0, boxes = 0;
+  while (up < nc || dn >= 0) {
+    int c;
+    if ((turn_up && up < nc) || dn < 0) c = up++; else c = dn--;
+    turn_up = !turn_up;
+    const double* bx = cbox + 16 * (size_t)c;
+    double lb0 = 0, lb1 = 0;
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      const double g0 = fmax(0.0, fmax(bx[k] - s0[k], s0[k] - bx[8 + k]));
+      const double g1 = fmax(0.0, fmax(bx[k] - s1[k], s1[k] - bx[8 + k]));
+      lb0 = fma(UW ? g0 : w[k] * g0, g0, lb0);
+      lb1 = fma(UW ? g1 : w[k] * g1, g1, lb1);
+    }
+    ++boxes;
+    const bool need = (a0 && lb0 <= thr0) || (a1 && lb1 <= thr1);
+    if (__ballot(need) == 0) continue;
+    const long long n0 = (long long)c * kChunk, n1 = min(T, n0 + kChunk);
+    for (long long pp = n0; pp < n1; ++pp) {
+      const double* nd = stree + 8 * pp;
+      nn_update<UW>(s0, nd, w, b10, b20, bi0, thr0, ru);
+      nn_update<UW>(s1, nd, w, b11, b21, bi1, thr1, ru);
+    }
+    scanned += (unsigned long long)(n1 - n0);
+  }
+  if (a0) { nn[l0] = bi0 == INT_MAX ? 0 : bi0; if (second) second[l0] = b20; }
+  if (a1) { nn[l1] = bi1 == INT_MAX ? 0 : bi1; if (second) second[l1] = b21; }
+  const unsigned long long act = __popcll(__ballot(a0)) + __popcll(__ballot(a1));
+  if (lane == 0) {
+    atomicAdd(&st->nn_pairs, scanned * act);
+    atomicAdd(&st->nn_box_tests, boxes * act);
+  }
+}
+
+#endif
+#include "tcmp_nn.h"
 
 // merge the per-split partial results: nearest index and the second-smallest distance
 template <bool UW>
@@ -841,6 +1043,14 @@ struct tcmp_handle {
   DBuf<unsigned char> cgoal;
   DBuf<int> nn, nsafe, nsteps, nbr, ncount, pidx, rwlist;
   DBuf<double> pd1, pd2;
+  // Morton-chunked snapshot
+  DBuf<unsigned long long> nkeys_in, skeys, ckeys_in, ckeys;
+  DBuf<int> nvals_in, svals, cvals_in, cperm;
+  DBuf<double> stree, cbox;
+  DBuf<float> cboxf, sboxf;
+  DBuf<int> chome;
+  DBuf<unsigned char> sort_tmp;
+  bool nn_brute = false;
   DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
@@ -940,6 +1150,47 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const double* tree, long
   return 0;
 }
 
+// Morton-chunked nearest over the plan's tree snapshot (T <= T_bound nodes on the device)
+int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_bound, int nb) {
+  hipLaunchKernelGGL(k_node_keys, dim3(std::min<unsigned>(grid_for(T_bound, 256), 4096)), dim3(256),
+                     0, h->stream, h->st, h->cfg.p, T_bound, h->nkeys_in.p, h->nvals_in.p);
+  HIPCHK(hipGetLastError());
+  size_t tb = h->sort_tmp.n;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
+                                            h->nvals_in.p, h->svals.p, (int)T_bound, 0, 64,
+                                            h->stream));
+  hipLaunchKernelGGL(k_nn_build_chunks, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
+                     h->st, h->cfg.p, h->svals.p, h->stree.p, h->cboxf.p);
+  HIPCHK(hipGetLastError());
+  const long long nsup_bound = (((T_bound + kNnC - 1) / kNnC) + kNnS - 1) / kNnS;
+  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(nsup_bound * 64, 256)), dim3(256), 0,
+                     h->stream, h->st, h->cboxf.p, h->sboxf.p);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
+                     h->ckeys_in.p, h->cvals_in.p);
+  HIPCHK(hipGetLastError());
+  tb = h->sort_tmp.n;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
+                                            h->cvals_in.p, h->cperm.p, nb, 0, 64, h->stream));
+  hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
+                     h->skeys.p, h->ckeys.p, nb, h->chome.p);
+  HIPCHK(hipGetLastError());
+  // one wave per candidate at a time; contiguous Morton-sorted runs per wave
+  const long long waves = std::min<long long>(nb, (long long)h->cu_count * 16);
+  const int per_wave = (int)((nb + waves - 1) / waves);
+  const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
+  if (P.uniform_w)
+    hipLaunchKernelGGL(k_nearest_wave<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
+                       h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
+                       per_wave, h->nn.p, h->second.p);
+  else
+    hipLaunchKernelGGL(k_nearest_wave<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
+                       h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
+                       per_wave, h->nn.p, h->second.p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   if (J.n <= 0) return 0;
   HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
@@ -1008,6 +1259,8 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMemcpy(h->edges.p, tcmp_geo_edges, sizeof(tcmp_geo_edges), hipMemcpyHostToDevice));
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
+  const char* nb_env = getenv("TCMP_NN_BRUTE");
+  h->nn_brute = nb_env && nb_env[0] == '1';
   *out = h;
   return 0;
 }
@@ -1025,6 +1278,14 @@ int tcmp_destroy(tcmp_handle* h) {
     b->release();
   h->pd1.release();
   h->pd2.release();
+  for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
+  for (auto* b : {&h->nvals_in, &h->svals, &h->cvals_in, &h->cperm}) b->release();
+  h->stree.release();
+  h->cbox.release();
+  h->cboxf.release();
+  h->sboxf.release();
+  h->chome.release();
+  h->sort_tmp.release();
   h->meta.release();
   h->cgoal.release();
   h->second.release();
@@ -1273,6 +1534,26 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->ncount.ensure(B);
   rc = rc ? rc : h->second.ensure(B);
   rc = rc ? rc : h->rwlist.ensure(B);
+  rc = rc ? rc : h->nkeys_in.ensure(N);
+  rc = rc ? rc : h->skeys.ensure(N);
+  rc = rc ? rc : h->nvals_in.ensure(N);
+  rc = rc ? rc : h->svals.ensure(N);
+  rc = rc ? rc : h->stree.ensure(N * 8);
+  rc = rc ? rc : h->cboxf.ensure(((N + kNnC - 1) / kNnC + 1) * 16);
+  rc = rc ? rc : h->sboxf.ensure(((N + kNnC * kNnS - 1) / (kNnC * kNnS) + 1) * 16);
+  rc = rc ? rc : h->chome.ensure(B);
+  rc = rc ? rc : h->ckeys_in.ensure(B);
+  rc = rc ? rc : h->ckeys.ensure(B);
+  rc = rc ? rc : h->cvals_in.ensure(B);
+  rc = rc ? rc : h->cperm.ensure(B);
+  if (!rc) {
+    size_t t1 = 0, t2 = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, h->nkeys_in.p, h->skeys.p, h->nvals_in.p,
+                                              h->svals.p, (int)N, 0, 64, h->stream));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, h->ckeys_in.p, h->ckeys.p, h->cvals_in.p,
+                                              h->cperm.p, (int)B, 0, 64, h->stream));
+    rc = h->sort_tmp.ensure(std::max(t1, t2));
+  }
   rc = rc ? rc : h->i0.ensure(2);
   if (rc) return rc;
   h->max_batch = cfg->max_batch;
@@ -1339,9 +1620,13 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
     HIPCHK(hipGetLastError());
   }
   // the snapshot holds at most 1 + (samples issued before this round) nodes
-  if (int rc = launch_nearest(h, P, h->cfg.p, 1 + h->samples_issued - nb, -1, h->cand.p, nb,
-                              h->nn.p, h->second.p))
-    return rc;
+  {
+    const long long T_bound = 1 + h->samples_issued - nb;
+    const int rc = h->nn_brute
+                       ? launch_nearest(h, P, h->cfg.p, T_bound, -1, h->cand.p, nb, h->nn.p, h->second.p)
+                       : launch_nearest_chunked(h, P, T_bound, nb);
+    if (rc) return rc;
+  }
   h->mark_end(F_NEAREST, e0);
   h->launches_nearest++;
   h->mark_begin(F_EDGES, &e0);
@@ -1460,6 +1745,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   r->ms_rewire = h->ms[F_REWIRE];
   r->ms_finish = h->ms[F_FINISH];
   r->launches_nearest = h->launches_nearest;
+  r->nn_box_tests = s.nn_box_tests;
   return 0;
 }
 
