@@ -10,7 +10,7 @@ import threading
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libtcmp.so")
+LIB_PATH = os.environ.get("TCMP_LIB_PATH", os.path.join(HERE, "libtcmp.so"))
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _i32p = ctypes.POINTER(ctypes.c_int32)

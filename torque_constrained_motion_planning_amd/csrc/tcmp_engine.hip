@@ -59,6 +59,8 @@ struct DevState {
   long long W, ni, K, first_fail;
   unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
   unsigned long long nn_box_tests;
+  long long ins_total;   // accepted edges of the current round (k_ins_scan)
+  long long ins_goal;    // lowest goal-reaching new node of the round (k_ins_write)
   int work_counter;
   int round_goal;
   int rw_count;
@@ -415,6 +417,7 @@ __global__ __launch_bounds__(256) void k_nearest_chunked(PlanParams P, DevState*
 
 #endif
 #include "tcmp_nn.h"
+#include "tcmp_insert.h"
 
 // merge the per-split partial results: nearest index and the second-smallest distance
 template <bool UW>
@@ -456,7 +459,10 @@ struct EdgeJob {
   double* last;             // stride 8
 };
 
-__global__ __launch_bounds__(256) void k_edges(EdgeJob J, PlanParams P, Scene sc, Geo g,
+#ifndef TCMP_EDGE_MINW
+#define TCMP_EDGE_MINW 2  // min waves per SIMD the register allocation must allow
+#endif
+__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanParams P, Scene sc, Geo g,
                                                DevState* st) {
   const int lane = lane_id();
   int e = -1, i = 0, n = 0;
@@ -1048,7 +1054,7 @@ struct tcmp_handle {
   DBuf<int> nvals_in, svals, cvals_in, cperm;
   DBuf<double> stree, cbox;
   DBuf<float> cboxf, sboxf;
-  DBuf<int> chome;
+  DBuf<int> chome, bcount, boff;
   DBuf<unsigned char> sort_tmp;
   bool nn_brute = false;
   DBuf<double> second;
@@ -1197,7 +1203,8 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   // persistent grid: ~2 edges per lane keeps refill useful; bounded by residency
   long long lanes = std::max<long long>(64, (J.n + 1) / 2);
   long long blocks = (lanes + 255) / 256;
-  const long long cap = (long long)h->cu_count * 4;  // 4 x 256-thread blocks per CU
+  // resident blocks: 256-thread blocks hold one wave per SIMD each
+  const long long cap = (long long)h->cu_count * std::max(2, TCMP_EDGE_MINW);
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
@@ -1285,6 +1292,8 @@ int tcmp_destroy(tcmp_handle* h) {
   h->cboxf.release();
   h->sboxf.release();
   h->chome.release();
+  h->bcount.release();
+  h->boff.release();
   h->sort_tmp.release();
   h->meta.release();
   h->cgoal.release();
@@ -1634,10 +1643,20 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   if (int rc = launch_edges(h, J, P)) return rc;
   h->mark_end(F_EDGES, e0);
   h->mark_begin(F_INSERT, &e0);
-  hipLaunchKernelGGL(k_insert, dim3(1), dim3(1024), 0, h->stream, P, h->st, tr, h->nn.p,
-                     h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->second.p,
-                     h->rwlist.p);
-  HIPCHK(hipGetLastError());
+  {
+    const int nblk = (int)grid_for(nb, 256);
+    if (int rc = h->bcount.ensure(nblk)) return rc;
+    if (int rc = h->boff.ensure(nblk)) return rc;
+    hipLaunchKernelGGL(k_ins_count, dim3(nblk), dim3(256), 0, h->stream, h->nsafe.p, nb,
+                       h->bcount.p);
+    hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
+                       h->boff.p);
+    hipLaunchKernelGGL(k_ins_write, dim3(nblk), dim3(256), 0, h->stream, P, h->st, tr, h->nn.p,
+                       h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->boff.p,
+                       h->second.p, h->rwlist.p);
+    hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, P, h->st, nb);
+    HIPCHK(hipGetLastError());
+  }
   h->mark_end(F_INSERT, e0);
   h->mark_begin(F_REWIRE, &e0);
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,

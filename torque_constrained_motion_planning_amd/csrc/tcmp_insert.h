@@ -1,0 +1,106 @@
+// tcmp_insert.h -- lane-ordered insertion of a round's accepted edges (rrt_star.py:173-180),
+// as a device-wide scan: count per 256-lane block, one-block scan of the counts, then every
+// block writes its nodes at (snapshot size + block offset + in-block rank).  Node order is
+// therefore lane order, exactly as the single-pass reference loop appends them.
+// Included by tcmp_engine.hip after the state types and k_insert.
+#pragma once
+
+__global__ __launch_bounds__(256) void k_ins_count(const int* nsafe, int nb, int* bcount) {
+  __shared__ int wc[4];
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const bool v = j < nb && nsafe[j] > 0;
+  const int c = (int)__popcll(__ballot(v));
+  if (lane_id() == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) bcount[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+
+__global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcount, int nblocks,
+                                                   int* boff) {
+  __shared__ int sc[1024];
+  const int tid = threadIdx.x;
+  int run = 0;
+  for (int b0 = 0; b0 < nblocks; b0 += 1024) {
+    const int b = b0 + tid;
+    const int v = b < nblocks ? bcount[b] : 0;
+    sc[tid] = v;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+      const int x = tid >= o ? sc[tid - o] : 0;
+      __syncthreads();
+      sc[tid] += x;
+      __syncthreads();
+    }
+    if (b < nblocks) boff[b] = run + sc[tid] - v;
+    run += sc[1023];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    st->ins_total = run;
+    st->ins_goal = LLONG_MAX;
+    st->rw_count = 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ins_write(PlanParams P, DevState* st, Tree tr,
+                                                   const int* nn, const double* cand,
+                                                   const unsigned char* cgoal, const int* nsafe,
+                                                   const int* nsteps, const double* last, int nb,
+                                                   const int* boff, const double* second,
+                                                   int* rwlist) {
+  __shared__ int wc[4];
+  const long long T = st->n_nodes;
+  const long long total = st->ins_total;
+  if (T + total > P.max_nodes) return;  // k_ins_final flags the overflow
+  const bool goal_open = st->goal_node < 0;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const bool v = j < nb && nsafe[j] > 0;
+  const uint64_t m = __ballot(v);
+  const int lane = lane_id(), w = threadIdx.x >> 6;
+  if (lane == 0) wc[w] = (int)__popcll(m);
+  __syncthreads();
+  int before = 0;
+  for (int i = 0; i < w; ++i) before += wc[i];
+  if (!v) return;
+  const long long idx = T + boff[blockIdx.x] + before + (int)__popcll(m & ((1ull << lane) - 1ull));
+  const int par = nn[j];
+  double pc[7], lq[7], tq[7];
+  load7(tr.cfg + 8 * (size_t)par, pc);
+  load7(last + 8 * (size_t)j, lq);
+  load7(cand + 8 * (size_t)j, tq);
+  const double d = distance(pc, lq, P.w);
+  double* dst = tr.cfg + 8 * idx;
+  store7(dst, lq);
+  dst[7] = tr.cfg[8 * (size_t)par + 7] + d;
+  tr.parent[idx] = par;
+  store7(tr.tgt + 8 * idx, tq);
+  tr.meta[idx] = make_int2(nsteps[j], nsafe[j]);
+  if (goal_open && cgoal[j] && distance(lq, P.goal, P.w) < P.goal_tol)
+    atomicMin(&st->ins_goal, idx);
+  // rewire bound (see k_insert): neighbour scan only if the second-nearest passes it
+  double e2 = 0;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const double dd = lq[k] - tq[k];
+    e2 = fma(P.uniform_w ? dd : P.w[k] * dd, dd, e2);
+  }
+  const double r = P.uniform_w ? P.radius / sqrt(P.w[0]) : P.radius;
+  const double t = sqrt(e2) + r;
+  if (second[j] < t * t * (1.0 + 1e-9) + 1e-300) rwlist[atomicAdd(&st->rw_count, 1)] = (int)idx;
+}
+
+__global__ void k_ins_final(PlanParams P, DevState* st, int nb) {
+  const long long T = st->n_nodes, total = st->ins_total;
+  st->snap = T;
+  if (T + total > P.max_nodes) {
+    st->overflow = 1;
+    st->new_count = 0;
+    st->rw_count = 0;
+  } else {
+    st->new_count = total;
+    st->n_nodes = T + total;
+    if (st->goal_node < 0 && st->ins_goal != LLONG_MAX) st->goal_node = st->ins_goal;
+  }
+  st->samples += nb;
+  st->round_goal = INT_MAX;
+}
