@@ -62,6 +62,7 @@ struct DevState {
   long long ins_total;   // accepted edges of the current round (k_ins_scan)
   long long ins_goal;    // lowest goal-reaching new node of the round (k_ins_write)
   int work_counter;
+  int nn_counter;
   int round_goal;
   int rw_count;
   int status;
@@ -1057,6 +1058,7 @@ struct tcmp_handle {
   DBuf<int> chome, bcount, boff;
   DBuf<unsigned char> sort_tmp;
   bool nn_brute = false;
+  int nn_waves_per_cu = 24;
   DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
@@ -1182,7 +1184,8 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
                      h->skeys.p, h->ckeys.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave
-  const long long waves = std::min<long long>(nb, (long long)h->cu_count * 16);
+  HIPCHK(hipMemsetAsync(&h->st->nn_counter, 0, sizeof(int), h->stream));
+  const long long waves = std::min<long long>(nb, (long long)h->cu_count * h->nn_waves_per_cu);
   const int per_wave = (int)((nb + waves - 1) / waves);
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   if (P.uniform_w)
@@ -1268,6 +1271,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
   const char* nb_env = getenv("TCMP_NN_BRUTE");
   h->nn_brute = nb_env && nb_env[0] == '1';
+  if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   *out = h;
   return 0;
 }

@@ -146,9 +146,8 @@ __global__ __launch_bounds__(256) void k_nearest_wave(PlanParams P, DevState* st
                                                       int per_wave, int* nn, double* second) {
   const int lane = lane_id();
   const long long gw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long jbeg = gw * per_wave;
-  if (jbeg >= nb) return;  // wave-uniform
-  const long long jend = min((long long)nb, jbeg + per_wave);
+  (void)gw;
+  (void)per_wave;
   const long long T = st->n_nodes;
   const int nch = (int)((T + kNnC - 1) / kNnC), nsup = (nch + kNnS - 1) / kNnS;
   double w[7];
@@ -156,7 +155,13 @@ __global__ __launch_bounds__(256) void k_nearest_wave(PlanParams P, DevState* st
   for (int k = 0; k < 7; ++k) w[k] = P.w[k];
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
   unsigned long long pairs = 0, tests = 0;
-  for (long long j = jbeg; j < jend; ++j) {
+  while (true) {
+    // dynamic queue over the Morton-sorted candidates: one atomic per candidate per wave
+    int jq = 0;
+    if (lane == 0) jq = atomicAdd(&st->nn_counter, 1);
+    jq = __shfl(jq, 0);
+    if (jq >= nb) break;
+    const long long j = jq;
     const int lj = cperm[j];
     double s[7];
     load7(cand + 8 * (size_t)lj, s);
@@ -195,6 +200,49 @@ __global__ __launch_bounds__(256) void k_nearest_wave(PlanParams P, DevState* st
       const double t = sqrt(wave_min(b1)) + ru;
       return t * t * (1.0 + 1e-9) + 1e-300;
     };
+    auto upd = [&](const double4 a, const double4 b) {
+      const double d0 = s[0] - a.x, d1 = s[1] - a.y, d2 = s[2] - a.z, d3 = s[3] - a.w,
+                   d4 = s[4] - b.x, d5 = s[5] - b.y, d6 = s[6] - b.z;
+      double dd;
+      if (UW) {
+        dd = d0 * d0;
+        dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
+        dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
+      } else {
+        dd = w[0] * (d0 * d0);
+        dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
+        dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
+      }
+      const int idx = (int)b.w;
+      if (dd < b1 || (dd == b1 && idx < bi)) {
+        b2 = b1;
+        b1 = dd;
+        bi = idx;
+      } else {
+        b2 = fmin(b2, dd);
+      }
+    };
+    // scan up to four chunks (-1 = none) with all their loads in flight before any use
+    auto scan4 = [&](int c0, int c1, int c2, int c3) {
+      const int cs[4] = {c0, c1, c2, c3};
+      double4 A[4], Bq[4];
+      bool val[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long n = (long long)cs[u] * kNnC + lane;
+        val[u] = cs[u] >= 0 && n < T;
+        if (val[u]) {
+          A[u] = *reinterpret_cast<const double4*>(stree + 8 * n);
+          Bq[u] = *reinterpret_cast<const double4*>(stree + 8 * n + 4);
+        }
+        if (cs[u] >= 0) pairs += (unsigned long long)min((long long)kNnC, T - (long long)cs[u] * kNnC);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (val[u]) upd(A[u], Bq[u]);
+      const double t = sqrt(wave_min(b1)) + ru;
+      return t * t * (1.0 + 1e-9) + 1e-300;
+    };
     double thr = scan(hc);
     for (int g = 0; g < nsup; g += 64) {
       const int sidx = zigzag(hs, g + lane, nsup);
@@ -212,10 +260,18 @@ __global__ __launch_bounds__(256) void k_nearest_wave(PlanParams P, DevState* st
         tests += (unsigned long long)min(kNnS, nch - S * kNnS);
         uint64_t cmask = __ballot(lbc <= thr);
         while (cmask) {
-          const int k = __builtin_ctzll(cmask);
-          cmask &= cmask - 1;
-          if (__shfl(lbc, k) > thr) continue;
-          thr = scan(S * kNnS + k);
+          // up to 4 chunks per pass: their node loads are independent, so all are in flight
+          // together; the threshold is refreshed once per pass
+          auto take = [&]() -> int {
+            while (cmask) {
+              const int k = __builtin_ctzll(cmask);
+              cmask &= cmask - 1;
+              if (__shfl(lbc, k) <= thr) return S * kNnS + k;
+            }
+            return -1;
+          };
+          const int ca = take(), cb = take(), cc = take(), cd = take();
+          if (ca >= 0) thr = scan4(ca, cb, cc, cd);
         }
       }
     }
