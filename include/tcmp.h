@@ -82,6 +82,18 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
                        int64_t n, int32_t torque_mode, double payload_mass, int64_t* first_fail,
                        double* tau);
 
+/* ---- goal IK ------------------------------------------------------------ */
+/* ikfast get_ik (ikfast_panda_arm.cpp:12839 -> ComputeIk :12770, free joint = joint7 :398),
+ * batched: poses n x 12 = panda_link8 in panda_link0 (rotation 9 row-major, then position 3,
+ * the eerot/eetrans of :12854-12862), free_q7 n values.  sols: n x 8 x 7 (the count[i]
+ * solutions of row i packed first, angles in (-pi, pi]); count: n.  Joint limits are NOT
+ * applied (the reference filters afterwards, ikfast.py:166). */
+int tcmp_ik(tcmp_handle* h, const double* poses, const double* free_q7, int64_t n, double* sols,
+            int32_t* count);
+
+/* ikfast get_fk (ikfast_panda_arm.cpp:12907 -> ComputeFk :307): q n x 7 -> poses n x 12. */
+int tcmp_fk(tcmp_handle* h, const double* q, int64_t n, double* poses);
+
 /* ---- the RRT* engine (rrt_star_force_aware, rrt_star.py:151-211) ------------------------ */
 typedef struct {
   double start[7];
@@ -120,6 +132,7 @@ typedef struct {
   double ms_finish;
   int64_t launches_nearest;
   uint64_t nn_box_tests;  /* (candidate, chunk-box) lower-bound tests of the pruned scan */
+  double ms_nn_scan;      /* the k_nearest_wave launches alone (part of ms_nearest) */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

@@ -57,6 +57,8 @@ def lib():
         L.orc_pair_pd.restype = ctypes.c_double
         L.orc_check_edge.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                      ctypes.c_int, _ip, _dp]
+        L.orc_fk8.argtypes = [_dp, _dp, _dp]
+        L.orc_ik8.argtypes = [_dp, _dp, ctypes.c_double, _dp, ctypes.POINTER(ctypes.c_int)]
         L.orc_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _dp]
         L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
                                   ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
@@ -135,6 +137,30 @@ def check_edge(q1, q2, obs, torque_mode, mass, cull=1):
     s = lib().orc_check_edge(_d(q1), _d(q2), _d(o) if len(o) else None, len(o),
                              int(torque_mode), float(mass), int(cull), ctypes.byref(ns), _d(last))
     return s, ns.value, last
+
+
+def fk8(q):
+    """T_0^8 (4x4) by the reference DH chain (rne.py:32-63)."""
+    q = _arr(q, (7,))
+    R = np.zeros(9)
+    p = np.zeros(3)
+    lib().orc_fk8(_d(q), _d(R), _d(p))
+    T = np.eye(4)
+    T[:3, :3] = R.reshape(3, 3)
+    T[:3, 3] = p
+    return T
+
+
+def ik8(T, q7):
+    """Closed-form IK of T_0^8 with joint 7 = q7: (solutions (k, 7), branch ids (k,))."""
+    T = np.asarray(T, dtype=np.float64)
+    R = np.ascontiguousarray(T[:3, :3]).reshape(9).copy()
+    p = np.ascontiguousarray(T[:3, 3]).copy()
+    sols = np.zeros(56)
+    valid = np.zeros(8, dtype=np.intc)
+    lib().orc_ik8(_d(R), _d(p), float(q7), _d(sols), valid.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    idx = np.nonzero(valid)[0]
+    return sols.reshape(8, 7)[idx], idx
 
 
 def philox_uniforms(seed, k):

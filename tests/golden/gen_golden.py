@@ -14,6 +14,10 @@ piece against Bullet is unpinned).
 Outputs (small npz fixtures, no pickles) in tests/golden/:
   rne_golden.npz       reference rne() torques, static and dynamic, payload 0/2/5 kg
   minjerk_golden.npz   reference minjerk_coefficients/minjerk_trajectory outputs
+  fk_golden.npz        reference DH forward kinematics panda_link0 -> panda_link8
+                       (X = rne.get_parent_to_child_transform(q, 0, 8) = inv(T_0^8),
+                       rne.py:46-63, and T = inv(X)): pins the
+                       FK the IK round trip is checked with (ikfast itself is unbuildable here)
   rrt_<name>.npz       full reference RRT* runs: RNG streams consumed, waypoints,
                        trajectory q/qd/qdd/psg (strided subsample for long ones)
 """
@@ -223,6 +227,20 @@ def gen_minjerk(path):
     np.savez_compressed(path, **out)
 
 
+def gen_fk(path):
+    rng = np.random.default_rng(77)
+    q = rng.uniform(LO, HI, size=(400, 7))
+    # a few structured rows: zeros, the holding pose, joint-limit corners
+    q[0] = 0.0
+    q[1] = TOP_HOLDING_LEFT_ARM
+    q[2] = LO
+    q[3] = HI
+    # get_parent_to_child_transform returns inv(T_0^8) (rne.py:63); keep it raw and its inverse
+    X = np.stack([ref_rne.get_parent_to_child_transform(list(r), 0, 8) for r in q])
+    T = np.stack([np.linalg.inv(x) for x in X])
+    np.savez_compressed(path, q=q, X=X, T=T)
+
+
 def boxes_scene(rng, n, avoid):
     """SURVEY 8d synthetic boxes: centres U([0.2,0.8]x[-0.6,0.6]x[0,0.8]), half U[0.03,0.12],
     axis aligned, rejected if any configuration in `avoid` collides."""
@@ -325,6 +343,10 @@ def search(name, rng, n_obs, mode, mass, exec_time, iters, seed, want_found=True
 
 
 def main():
+    if "--only-fk" in sys.argv:
+        gen_fk(os.path.join(HERE, "fk_golden.npz"))
+        return
+    gen_fk(os.path.join(HERE, "fk_golden.npz"))
     gen_rne(os.path.join(HERE, "rne_golden.npz"))
     gen_minjerk(os.path.join(HERE, "minjerk_golden.npz"))
     rng = np.random.default_rng(1234)

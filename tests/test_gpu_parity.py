@@ -208,3 +208,74 @@ def test_batched_frontier_vs_oracle(eng, batch, n_obs, mode, mass):
         assert np.abs(raw["qdd"] - ref["qdd"]).max() < 1e-9
     else:
         assert r.status == ref["status"]
+
+
+# ---- goal IK ------------------------------------------------------------
+def test_fk_golden(eng):
+    """tcmp_fk == the reference DH chain (rne.py:46-63 via fk_golden.npz)."""
+    z = np.load(os.path.join(GOLDEN, "fk_golden.npz"))
+    P = eng.fk(z["q"])
+    T = z["T"]
+    assert np.abs(P[:, :9] - T[:, :3, :3].reshape(-1, 9)).max() < 1e-12
+    assert np.abs(P[:, 9:] - T[:, :3, 3]).max() < 1e-12
+
+
+def test_ik_vs_oracle(eng):
+    """tcmp_ik == the oracle solver, branch by branch, and every solution maps back through
+    the reference FK; the generating configuration is among the solutions."""
+    rng = np.random.default_rng(31)
+    q = rand_q(rng, 3000)
+    T = np.stack([O.fk8(r) for r in q])
+    free = q[:, 6].copy()
+    free[::3] = rng.uniform(LO[6], HI[6], size=len(free[::3]))  # other free values too
+    sols, cnt = eng.ik(T, free)
+    back = eng.fk(sols.reshape(-1, 7)).reshape(len(q), 8, 12)
+    hit = 0
+    for i in range(len(q)):
+        ref, _ = O.ik8(T[i], free[i])
+        assert cnt[i] == len(ref)
+        if cnt[i]:
+            assert np.abs(sols[i, :cnt[i]] - ref).max() < 1e-9
+            Tb = back[i, :cnt[i]]
+            assert np.abs(Tb[:, :9] - T[i, :3, :3].reshape(9)).max() < 1e-9
+            assert np.abs(Tb[:, 9:] - T[i, :3, 3]).max() < 1e-9
+        if i % 3 and cnt[i]:
+            d = (sols[i, :cnt[i]] - q[i] + np.pi) % (2 * np.pi) - np.pi
+            hit += np.abs(d).max(1).min() < 1e-8
+    assert hit == sum(1 for i in range(len(q)) if i % 3)
+
+
+def test_planner_fn_force_aware_end_to_end(eng):
+    """panda_primitives.planner_fn_force_aware: top grasp -> GPU IK -> RRT* -> Trajectory.
+    The goal conf must put the grasp target on the requested gripper pose."""
+    import random as pyrandom
+    from torque_constrained_motion_planning_amd import ik as IK
+    from torque_constrained_motion_planning_amd import panda_primitives as PP
+    from torque_constrained_motion_planning_amd.scene import Box, PandaRobot, Payload
+    from torque_constrained_motion_planning_amd.utils import Problem
+    np.random.seed(3)
+    pyrandom.seed(3)
+    robot = PandaRobot()
+    table = Box(center=(0.5, 0.0, -0.02), size=(0.6, 1.0, 0.04))
+    payload = Payload.coke(1.0)
+    problem = Problem(robot, [table], payload, 1.0, 1.0, torque_test="rne")
+    start = IK.TOP_HOLDING_LEFT_ARM
+    pose = ((0.45, 0.1, 0.2), IK.quat_from_euler((0, 0, 0)))
+    grasp_conf = IK.grasp_conf_for_pose(problem, start, pose, engine=eng)
+    assert grasp_conf is not None
+    grasp = IK.get_top_grasp(payload)
+    gripper = IK.to_matrix(IK.multiply(pose, IK.invert(grasp.value)))
+    P = eng.fk(np.array([grasp_conf]))[0]
+    T8 = np.eye(4)
+    T8[:3, :3] = P[:9].reshape(3, 3)
+    T8[:3, 3] = P[9:]
+    assert np.abs(T8 @ IK.EE_TO_TOOL - gripper).max() < 1e-9
+    np.random.seed(4)
+    pyrandom.seed(4)
+    traj = PP.planner_fn_force_aware(start, pose, problem)
+    if traj is not None:
+        last = np.array(traj.path[-1].values)
+        P = eng.fk(last[None])[0]
+        T8[:3, :3] = P[:9].reshape(3, 3)
+        T8[:3, 3] = P[9:]
+        assert np.abs(T8 @ IK.EE_TO_TOOL - gripper).max() < 1e-6

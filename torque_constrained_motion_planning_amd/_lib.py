@@ -26,7 +26,7 @@ EXPORTS = [
     "tcmp_set_scene", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
-    "tcmp_plan_fetch", "tcmp_plan_tree",
+    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk",
 ]
 
 
@@ -54,7 +54,7 @@ class PlanResult(ctypes.Structure):
         ("ms_nearest", ctypes.c_double), ("ms_edges", ctypes.c_double),
         ("ms_insert", ctypes.c_double), ("ms_rewire", ctypes.c_double),
         ("ms_finish", ctypes.c_double), ("launches_nearest", ctypes.c_int64),
-        ("nn_box_tests", ctypes.c_uint64),
+        ("nn_box_tests", ctypes.c_uint64), ("ms_nn_scan", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -100,6 +100,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
+        L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
+        L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
         _lib = L
         return L
 
@@ -115,6 +117,15 @@ def _rows(x, name="array"):
     if a.shape[-1] != 7:
         raise ValueError("%s must have 7 columns, got shape %s" % (name, a.shape))
     return a.reshape(-1, 7)
+
+
+def pose_rows(poses):
+    """(n, 4, 4) / (4, 4) homogeneous or (n, 12) rows -> contiguous (n, 12)."""
+    a = np.asarray(poses, dtype=np.float64)
+    if a.shape[-2:] == (4, 4):
+        a = a.reshape(-1, 4, 4)
+        a = np.concatenate([a[:, :3, :3].reshape(-1, 9), a[:, :3, 3]], axis=1)
+    return np.ascontiguousarray(a.reshape(-1, 12))
 
 
 class Engine:
@@ -159,6 +170,26 @@ class Engine:
         self._check(self.L.tcmp_rne_batch(self.h, _d(q), _d(qd), _d(qdd), len(q),
                                           float(payload_mass), _d(tau)))
         return tau
+
+    def ik(self, poses, free_q7):
+        """ikfast get_ik, batched: poses (n, 12) or (n, 4, 4) of panda_link8 in panda_link0,
+        free_q7 (n,).  Returns (sols (n, 8, 7), count (n,)); row i has count[i] solutions."""
+        poses = pose_rows(poses)
+        free_q7 = np.ascontiguousarray(np.asarray(free_q7, dtype=np.float64).reshape(-1))
+        if len(free_q7) != len(poses):
+            raise ValueError("one free value per pose")
+        sols = np.zeros((len(poses), 8, 7))
+        cnt = np.zeros(len(poses), dtype=np.int32)
+        self._check(self.L.tcmp_ik(self.h, _d(poses), _d(free_q7), len(poses), _d(sols),
+                                   cnt.ctypes.data_as(_i32p)))
+        return sols, cnt
+
+    def fk(self, q):
+        """ikfast get_fk: q (n, 7) -> (n, 12) rows (rotation row-major, position)."""
+        q = _rows(q, "q")
+        out = np.zeros((len(q), 12))
+        self._check(self.L.tcmp_fk(self.h, _d(q), len(q), _d(out)))
+        return out
 
     def torque_ok(self, q, mode, mass, qd=None, qdd=None):
         q = _rows(q, "q")

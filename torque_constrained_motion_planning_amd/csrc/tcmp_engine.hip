@@ -67,6 +67,7 @@ struct DevState {
   int rw_count;
   int status;
   int overflow;
+  int nn_queue[8];       // per-XCD work queues of k_nearest_wave32
 };
 
 struct PlanParams {
@@ -418,7 +419,9 @@ __global__ __launch_bounds__(256) void k_nearest_chunked(PlanParams P, DevState*
 
 #endif
 #include "tcmp_nn.h"
+#include "tcmp_nn32.h"
 #include "tcmp_insert.h"
+#include "tcmp_ik.h"
 
 // merge the per-split partial results: nearest index and the second-smallest distance
 template <bool UW>
@@ -1022,7 +1025,8 @@ struct DBuf {
   }
 };
 
-enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_COUNT };
+// F_NNSCAN times the k_nearest_wave launch alone (inside F_NEAREST, not added to totals)
+enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_NNSCAN, F_COUNT };
 
 struct EventPair {
   hipEvent_t a, b;
@@ -1054,6 +1058,8 @@ struct tcmp_handle {
   DBuf<unsigned long long> nkeys_in, skeys, ckeys_in, ckeys;
   DBuf<int> nvals_in, svals, cvals_in, cperm;
   DBuf<double> stree, cbox;
+  DBuf<float> stree32;
+  bool nn_fp32 = true;
   DBuf<float> cboxf, sboxf;
   DBuf<int> chome, bcount, boff;
   DBuf<unsigned char> sort_tmp;
@@ -1070,7 +1076,7 @@ struct tcmp_handle {
   // timing
   std::vector<EventPair> ev_used;
   std::vector<hipEvent_t> ev_pool;
-  double ms[F_COUNT] = {0, 0, 0, 0, 0};
+  double ms[F_COUNT] = {};
   long long launches_nearest = 0;
   int edge_blocks = 0;
 
@@ -1168,7 +1174,7 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
                                             h->nvals_in.p, h->svals.p, (int)T_bound, 0, 64,
                                             h->stream));
   hipLaunchKernelGGL(k_nn_build_chunks, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     h->st, h->cfg.p, h->svals.p, h->stree.p, h->cboxf.p);
+                     h->st, h->cfg.p, h->svals.p, h->stree.p, h->stree32.p, h->cboxf.p);
   HIPCHK(hipGetLastError());
   const long long nsup_bound = (((T_bound + kNnC - 1) / kNnC) + kNnS - 1) / kNnS;
   hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(nsup_bound * 64, 256)), dim3(256), 0,
@@ -1185,10 +1191,21 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave
   HIPCHK(hipMemsetAsync(&h->st->nn_counter, 0, sizeof(int), h->stream));
+  HIPCHK(hipMemsetAsync(h->st->nn_queue, 0, sizeof(int) * 8, h->stream));
   const long long waves = std::min<long long>(nb, (long long)h->cu_count * h->nn_waves_per_cu);
   const int per_wave = (int)((nb + waves - 1) / waves);
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
-  if (P.uniform_w)
+  hipEvent_t e0;
+  h->mark_begin(F_NNSCAN, &e0);
+  if (h->nn_fp32 && P.uniform_w)
+    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
+                       h->chome.p, nb, h->nn.p, h->second.p);
+  else if (h->nn_fp32)
+    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
+                       h->chome.p, nb, h->nn.p, h->second.p);
+  else if (P.uniform_w)
     hipLaunchKernelGGL(k_nearest_wave<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
                        h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
                        per_wave, h->nn.p, h->second.p);
@@ -1197,6 +1214,7 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
                        h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
                        per_wave, h->nn.p, h->second.p);
   HIPCHK(hipGetLastError());
+  h->mark_end(F_NNSCAN, e0);
   return 0;
 }
 
@@ -1272,6 +1290,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   const char* nb_env = getenv("TCMP_NN_BRUTE");
   h->nn_brute = nb_env && nb_env[0] == '1';
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
+  if (const char* e = getenv("TCMP_NN_FP32")) h->nn_fp32 = e[0] != '0';
   *out = h;
   return 0;
 }
@@ -1292,6 +1311,7 @@ int tcmp_destroy(tcmp_handle* h) {
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
   for (auto* b : {&h->nvals_in, &h->svals, &h->cvals_in, &h->cperm}) b->release();
   h->stree.release();
+  h->stree32.release();
   h->cbox.release();
   h->cboxf.release();
   h->sboxf.release();
@@ -1352,6 +1372,50 @@ int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const doub
                      h->s2.p, (long long)n, payload_mass, h->s3.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(tau, h->s3.p, (size_t)n * 7 * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_ik(tcmp_handle* h, const double* poses, const double* free_q7, int64_t n, double* sols,
+            int32_t* count) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!poses || !free_q7 || !sols || !count)))
+    return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = h->s0.ensure((size_t)n * 12);
+  rc = rc ? rc : h->s1.ensure((size_t)n);
+  rc = rc ? rc : h->s2.ensure((size_t)n * 56);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->s0.p, poses, (size_t)n * 12 * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipMemcpyAsync(h->s1.p, free_q7, (size_t)n * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  hipLaunchKernelGGL(k_ik, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->s0.p, h->s1.p,
+                     (long long)n, h->s2.p, h->i0.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(sols, h->s2.p, (size_t)n * 56 * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipMemcpyAsync(count, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_fk(tcmp_handle* h, const double* q, int64_t n, double* poses) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!q || !poses))) return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = h->s0.ensure((size_t)n * 7);
+  rc = rc ? rc : h->s1.ensure((size_t)n * 12);
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->s0.p, q, (size_t)n * 7 * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  hipLaunchKernelGGL(k_fk8, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->s0.p,
+                     (long long)n, h->s1.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(poses, h->s1.p, (size_t)n * 12 * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
@@ -1552,6 +1616,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->nvals_in.ensure(N);
   rc = rc ? rc : h->svals.ensure(N);
   rc = rc ? rc : h->stree.ensure(N * 8);
+  rc = rc ? rc : h->stree32.ensure(N * 8);
   rc = rc ? rc : h->cboxf.ensure(((N + kNnC - 1) / kNnC + 1) * 16);
   rc = rc ? rc : h->sboxf.ensure(((N + kNnC * kNnS - 1) / (kNnC * kNnS) + 1) * 16);
   rc = rc ? rc : h->chome.ensure(B);
@@ -1769,6 +1834,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   r->ms_finish = h->ms[F_FINISH];
   r->launches_nearest = h->launches_nearest;
   r->nn_box_tests = s.nn_box_tests;
+  r->ms_nn_scan = h->ms[F_NNSCAN];
   return 0;
 }
 

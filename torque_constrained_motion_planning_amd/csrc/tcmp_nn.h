@@ -4,6 +4,7 @@
 // Layout, rebuilt once per round from the snapshot (k_node_keys + radix sort + the two
 // build kernels below):
 //   stree [T][8] f64   nodes in Morton order: q0..q6, original node index
+//   stree32 [T][8] f32 the same coordinates rounded to fp32 (k_nearest_wave32's first pass)
 //   cbox  [T/64][16]   f32 bounds of each 64-node chunk (lo rounded down, hi rounded up)
 //   sbox  [T/4096][16] f32 bounds of each super-chunk (64 chunks)
 // A wave takes Morton-sorted candidates one at a time: it scans the candidate's home chunk
@@ -21,7 +22,7 @@ constexpr int kNnS = 64;              // chunks per super-chunk
 
 __global__ __launch_bounds__(256) void k_nn_build_chunks(DevState* st, const double* cfg,
                                                          const int* svals, double* stree,
-                                                         float* cbox) {
+                                                         float* stree32, float* cbox) {
   const long long T = st->n_nodes;
   if ((long long)blockIdx.x * 256 >= T) return;  // block-uniform
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
@@ -32,6 +33,9 @@ __global__ __launch_bounds__(256) void k_nn_build_chunks(DevState* st, const dou
     load7(cfg + 8 * (size_t)n, q);
     store7(stree + 8 * p, q);
     stree[8 * p + 7] = (double)n;
+    float4* d32 = reinterpret_cast<float4*>(stree32 + 8 * p);
+    d32[0] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
+    d32[1] = make_float4((float)q[4], (float)q[5], (float)q[6], 0.f);
 #pragma unroll
     for (int k = 0; k < 7; ++k) { lo[k] = q[k]; hi[k] = q[k]; }
   } else {

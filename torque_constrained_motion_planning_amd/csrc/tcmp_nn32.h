@@ -1,0 +1,210 @@
+// tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with an fp32
+// first pass.  Included by tcmp_engine.hip after tcmp_nn.h.
+//
+// Every (candidate, node) pair is first evaluated in fp32 on stree32 (half the bytes of the
+// fp64 rows, twice the VALU rate).  A node is re-evaluated exactly in fp64 (the same
+// arithmetic as k_nearest_wave, so the winner and its distance are bit-identical) only when
+// its fp32 value r32 could belong to a node at least as close as the wave's current best m:
+//
+//   |q| <= kNnCoordMax on the search path (joint-limit box), so each fp32 coordinate
+//   difference is within e = 4 u kNnCoordMax of the exact one (u = 2^-24), and with
+//   D = exact weighted distance, E = e sqrt(sum w):   r32 <= (1 + g) (D + E)^2,  g = 16 u.
+//   Refine iff r32 <= R(m) = (1 + g)(sqrt(m) + E)^2 (rounded up, with slack).
+//
+// Nodes that are not refined feed the second-smallest distance through the matching lower
+// bound LB(r32) = (sqrt(r32 / (1 + g)) - E)^2, so `second` is a lower bound of the exact value:
+// k_ins_write's rewire flag (a "may need the neighbour scan" test) stays conservative, and the
+// neighbour scan itself is exact.  Pruning uses the exact fp64 best, as before.
+//
+// Work distribution: eight queues, one per XCD, each over a contiguous eighth of the
+// Morton-sorted candidates; a wave pulls from its own XCD's queue (HW_REG_XCC_ID) so the
+// nodes one XCD touches stay in its L2, and moves on to the next queue when it runs dry.
+#pragma once
+
+constexpr double kNnU32 = 5.9604644775390625e-08;  // 2^-24
+constexpr double kNnCoordMax = 8.0;                 // > joint-limit magnitude (3.7525)
+constexpr double kNnE = 4.0 * kNnU32 * kNnCoordMax;
+constexpr double kNnG = 16.0 * kNnU32;
+
+__device__ __forceinline__ unsigned xcc_id() {
+  unsigned x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+
+template <bool UW>
+__global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* st,
+                                                        const double* stree,
+                                                        const float* stree32, const float* cbox,
+                                                        const float* sbox, const double* cand,
+                                                        const int* cperm, const int* home, int nb,
+                                                        int* nn, double* second) {
+  const int lane = lane_id();
+  const long long T = st->n_nodes;
+  const int nch = (int)((T + kNnC - 1) / kNnC), nsup = (nch + kNnS - 1) / kNnS;
+  double w[7], wsum = 0;
+  float w32[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    w[k] = P.w[k];
+    w32[k] = (float)w[k];
+    wsum += w[k];
+  }
+  const double E = kNnE * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
+  const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
+  unsigned long long pairs = 0, tests = 0;
+  int qi = (int)xcc_id(), tried = 0;
+  while (true) {
+    int jq = -1;
+    while (tried < 8) {
+      const int lo = (int)((long long)nb * qi / 8), hi = (int)((long long)nb * (qi + 1) / 8);
+      int t = 0;
+      if (lane == 0) t = atomicAdd(&st->nn_queue[qi], 1);
+      t = __shfl(t, 0);
+      if (lo + t < hi) {
+        jq = lo + t;
+        break;
+      }
+      qi = (qi + 1) & 7;
+      ++tried;
+    }
+    if (jq < 0) break;
+    const int lj = cperm[jq];
+    double s[7];
+    load7(cand + 8 * (size_t)lj, s);
+    float s32[7];
+#pragma unroll
+    for (int k = 0; k < 7; ++k) s32[k] = (float)s[k];
+    const int hc = min(nch - 1, home[jq] / kNnC);
+    const int hs = hc / kNnS;
+    double b1 = INFINITY, b2 = INFINITY;
+    int bi = INT_MAX;
+    float r2 = INFINITY;   // smallest fp32 value among this lane's unrefined nodes
+    float Rf = INFINITY;   // refine threshold R(m) (wave-uniform)
+    auto refine = [&](long long n) {
+      const double* nd = stree + 8 * n;
+      const double4 a = *reinterpret_cast<const double4*>(nd);
+      const double4 b = *reinterpret_cast<const double4*>(nd + 4);
+      const double d0 = s[0] - a.x, d1 = s[1] - a.y, d2 = s[2] - a.z, d3 = s[3] - a.w,
+                   d4 = s[4] - b.x, d5 = s[5] - b.y, d6 = s[6] - b.z;
+      double dd;
+      if (UW) {
+        dd = d0 * d0;
+        dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
+        dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
+      } else {
+        dd = w[0] * (d0 * d0);
+        dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
+        dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
+      }
+      const int idx = (int)b.w;
+      if (dd < b1 || (dd == b1 && idx < bi)) {
+        b2 = b1;
+        b1 = dd;
+        bi = idx;
+      } else {
+        b2 = fmin(b2, dd);
+      }
+    };
+    auto upd = [&](const float4 a, const float4 b, long long n) {
+      const float d0 = s32[0] - a.x, d1 = s32[1] - a.y, d2 = s32[2] - a.z, d3 = s32[3] - a.w,
+                  d4 = s32[4] - b.x, d5 = s32[5] - b.y, d6 = s32[6] - b.z;
+      float r;
+      if (UW) {
+        r = d0 * d0;
+        r = fmaf(d1, d1, r); r = fmaf(d2, d2, r); r = fmaf(d3, d3, r);
+        r = fmaf(d4, d4, r); r = fmaf(d5, d5, r); r = fmaf(d6, d6, r);
+      } else {
+        r = w32[0] * (d0 * d0);
+        r = fmaf(w32[1] * d1, d1, r); r = fmaf(w32[2] * d2, d2, r); r = fmaf(w32[3] * d3, d3, r);
+        r = fmaf(w32[4] * d4, d4, r); r = fmaf(w32[5] * d5, d5, r); r = fmaf(w32[6] * d6, d6, r);
+      }
+      if (r <= Rf) refine(n);
+      else r2 = fminf(r2, r);
+    };
+    // refresh the pruning threshold and the refine threshold from the exact best
+    auto refresh = [&]() {
+      const double m = wave_min(b1);
+      const double sm = sqrt(m);
+      const double t = sm + ru;
+      const double R = (1.0 + kNnG) * (sm * (1.0 + 1e-12) + E) * (sm * (1.0 + 1e-12) + E) *
+                       (1.0 + 1e-7);
+      Rf = __double2float_ru(R);
+      return t * t * (1.0 + 1e-9) + 1e-300;
+    };
+    auto scan4 = [&](int c0, int c1, int c2, int c3) {
+      const int cs[4] = {c0, c1, c2, c3};
+      float4 A[4], Bq[4];
+      bool val[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const long long n = (long long)cs[u] * kNnC + lane;
+        val[u] = cs[u] >= 0 && n < T;
+        if (val[u]) {
+          A[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n);
+          Bq[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n + 4);
+        }
+        if (cs[u] >= 0) pairs += (unsigned long long)min((long long)kNnC, T - (long long)cs[u] * kNnC);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (val[u]) upd(A[u], Bq[u], (long long)cs[u] * kNnC + lane);
+      return refresh();
+    };
+    double thr;
+    {
+      // home chunk: R = inf, every node exact
+      const long long n = (long long)hc * kNnC + lane;
+      if (n < T) refine(n);
+      pairs += (unsigned long long)min((long long)kNnC, T - (long long)hc * kNnC);
+      thr = refresh();
+    }
+    for (int g = 0; g < nsup; g += 64) {
+      const int sidx = zigzag(hs, g + lane, nsup);
+      const double lbs = sidx >= 0 ? box_lb<UW>(sbox + 16 * (size_t)sidx, s, w) : INFINITY;
+      tests += (unsigned long long)min(64, nsup - g);
+      uint64_t smask = __ballot(lbs <= thr);
+      while (smask) {
+        const int i = __builtin_ctzll(smask);
+        smask &= smask - 1;
+        if (__shfl(lbs, i) > thr) continue;
+        const int S = __shfl(sidx, i);
+        const int c = S * kNnS + lane;
+        const bool cv = c < nch && c != hc;
+        const double lbc = cv ? box_lb<UW>(cbox + 16 * (size_t)c, s, w) : INFINITY;
+        tests += (unsigned long long)min(kNnS, nch - S * kNnS);
+        uint64_t cmask = __ballot(lbc <= thr);
+        while (cmask) {
+          auto take = [&]() -> int {
+            while (cmask) {
+              const int k = __builtin_ctzll(cmask);
+              cmask &= cmask - 1;
+              if (__shfl(lbc, k) <= thr) return S * kNnS + k;
+            }
+            return -1;
+          };
+          const int ca = take(), cb = take(), cc = take(), cd = take();
+          if (ca >= 0) thr = scan4(ca, cb, cc, cd);
+        }
+      }
+    }
+    const double m = wave_min(b1);
+    const int wi = wave_min_int(b1 == m ? bi : INT_MAX);
+    const bool winner = (b1 == m) && (bi == wi);
+    double lb2 = INFINITY;
+    if (r2 < INFINITY) {
+      const double t = sqrt((double)r2 / (1.0 + kNnG)) - E;
+      lb2 = t > 0.0 ? t * t * (1.0 - 1e-7) : 0.0;
+    }
+    const double mine = winner ? fmin(b2, lb2) : fmin(fmin(b1, b2), lb2);
+    const double sec = wave_min(mine);
+    if (lane == 0) {
+      nn[lj] = wi == INT_MAX ? 0 : wi;
+      if (second) second[lj] = sec;
+    }
+  }
+  if (lane == 0) {
+    atomicAdd(&st->nn_pairs, pairs);
+    atomicAdd(&st->nn_box_tests, tests);
+  }
+}

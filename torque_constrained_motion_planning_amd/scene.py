@@ -74,12 +74,27 @@ class Box:
 class Payload:
     """Grasped object: mass (get_mass) and a cylinder/box shape for top grasps."""
 
-    def __init__(self, mass, radius=0.015, height=0.05, pose=None, name="payload"):
+    def __init__(self, mass, radius=0.015, height=0.05, pose=None, name="payload",
+                 center=(0.0, 0.0, 0.0), size=None):
         self.mass = float(mass)
         self.radius = float(radius)
         self.height = float(height)
         self.pose = pose
         self.name = name
+        # AABB of the collision shape in the body frame (approximate_as_prism, utils.py:2762):
+        # centre and full extents (w, l, h).  A cylinder's extents are (2r, 2r, h)
+        # (vertices_from_data, utils.py:2690-2695); a box passes size=(w, l, h).
+        self.center = np.asarray(center, dtype=np.float64).reshape(3)
+        if size is None:
+            size = (2 * self.radius, 2 * self.radius, self.height)
+        self.size = np.asarray(size, dtype=np.float64).reshape(3)
+
+    @classmethod
+    def coke(cls, mass):
+        """src/models/coke.urdf: cylinder r=0.015, length 0.05 at the link origin, inertial
+        origin z=-0.023.  pybullet reports base poses and collision frames relative to the
+        inertial frame, so the shape centre sits at +0.023 in the pose frame."""
+        return cls(mass, radius=0.015, height=0.05, name="coke", center=(0.0, 0.0, 0.023))
 
 
 def get_mass(body):
