@@ -38,6 +38,9 @@ int tcmp_destroy(tcmp_handle* h);
 const char* tcmp_last_error(void);
 int tcmp_device_count(int* n);
 int tcmp_version(void);
+/* profiling builds (-DTCMP_PROF) only: k_edges clock breakdown accumulated since create
+ * (total, work fetch, collision, torque, bookkeeping, tier-4 exact), n <= 8; zeros otherwise. */
+int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n);
 
 /* Fixed obstacles (replaces Problem.fixed bodies + pybullet getClosestPoints,
  * utils.py:3165-3218 / 2833-2849).  n_obs oriented boxes, 15 doubles each:

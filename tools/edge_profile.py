@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""k_edges clock breakdown on the C3 workload (profiling build libtcmp_prof.so, -DTCMP_PROF).
+
+usage: TCMP_LIB_PATH=torque_constrained_motion_planning_amd/libtcmp_prof.so \
+       python tools/edge_profile.py [n_queries]
+Prints, per query, the share of wave clocks k_edges spends fetching work, in the collision
+check (and its tier-4 exact part), in the torque check and in bookkeeping.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from torque_constrained_motion_planning_amd import _lib  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 3
+    eng = _lib.Engine(0)
+    obs, goal = bench.make_query(1234, engine=eng)
+    prev = [0] * 4
+    for q in range(n):
+        r, _ = bench.run_query(eng, obs, goal, 1_000_000, 262144, 1234 + q)
+        c = eng.debug_counters(12)
+        ex = [a - b for a, b in zip(c[8:12], prev)]
+        prev = c[8:12]
+        tot = max(1, c[0])
+        print(json.dumps({"query": q, "ms_edges": r.ms_edges, "total_clk": c[0],
+                          "fetch": c[1] / tot, "collision": c[2] / tot, "torque": c[3] / tot,
+                          "tail": c[4] / tot, "exact_in_collision": c[5] / tot,
+                          "sincos": c[6] / tot, "tiers123_in_collision": c[7] / tot,
+                          "exact32_box_exit": ex[0], "exact32_facets_would_exit": ex[1],
+                          "exact32_full": ex[2], "exact32_degenerate": ex[3],
+                          "edge_steps": r.edge_steps, "pairs_sat": r.pairs_sat,
+                          "pairs_exact": r.pairs_exact}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -138,6 +138,7 @@ def link_data(stl, flip_z_pi):
         for a, b in ((0, 1), (1, 2), (0, 2)):
             adj.setdefault(tuple(sorted((int(s[a]), int(s[b])))), []).append(tri_plane[ti])
     dirs = []
+    eidx = []
     for (a, b), fs in sorted(adj.items()):
         assert len(fs) == 2, "non-manifold hull edge"
         if fs[0] == fs[1]:
@@ -145,10 +146,11 @@ def link_data(stl, flip_z_pi):
         e = v[b] - v[a]
         e = e / np.linalg.norm(e)
         dirs.append(np.concatenate([e, v[a], planes[fs[0], :3], planes[fs[1], :3]]))
+        eidx.append([a, b, fs[0], fs[1]])
     dirs = np.array(dirs)
     c, R, half = obb_fit(v)
     ih = inner_box(c, R, half, planes[:, [0, 1, 2, 3]])
-    return dict(verts=v, planes=planes, edges=dirs, obb_c=c, obb_R=R, obb_half=half,
+    return dict(verts=v, planes=planes, edges=dirs, edge_idx=np.array(eidx), obb_c=c, obb_R=R, obb_half=half,
                 in_half=ih, hull_volume=h.volume)
 
 
@@ -206,6 +208,12 @@ def main():
             vals = list(p[0:3]) + [0.0] + list(p[3:6]) + [0.0] + list(p[6:9]) + [0.0] + list(p[9:12]) + [0.0]
             L.append("  " + ", ".join(fmt(x) for x in vals) + ",")
     L.append("};")
+    L.append("/* hull edges as indices: va vb (global vertex rows) f1 f2 (global plane rows) */")
+    L.append("TCMP_GEO_QUAL unsigned short tcmp_geo_edge_idx[TCMP_TOTAL_EDGES * 4] = {")
+    for i, d in enumerate(links):
+        for a, b, f1, f2 in d["edge_idx"]:
+            L.append("  %d, %d, %d, %d," % (a + ov[i], b + ov[i], f1 + of[i], f2 + of[i]))
+    L.append("};")
     L.append("/* per link box data: obb centre(3) axes R row-major (9, columns = box axes) "
              "outer half(3) inner half(3) -> 18 doubles */")
     L.append("TCMP_GEO_QUAL double tcmp_geo_boxes[TCMP_NLINKS * 18] = {")
@@ -221,6 +229,8 @@ def main():
              verts=np.concatenate([d["verts"] for d in links]),
              planes=np.concatenate([d["planes"] for d in links]),
              edges=np.concatenate([d["edges"] for d in links]),
+             edge_idx=np.concatenate([d["edge_idx"] + [ov[i], ov[i], of[i], of[i]]
+                                      for i, d in enumerate(links)]),
              vert_off=ov, plane_off=of, edge_off=oe,
              boxes=np.array([np.concatenate([d["obb_c"], d["obb_R"].reshape(-1), d["obb_half"],
                                              d["in_half"]]) for d in links]),

@@ -26,7 +26,7 @@ EXPORTS = [
     "tcmp_set_scene", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
-    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk",
+    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk", "tcmp_debug_counters",
 ]
 
 
@@ -102,6 +102,7 @@ def load_library(path=LIB_PATH):
         L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
         L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
         L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
+        L.tcmp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
         _lib = L
         return L
 
@@ -183,6 +184,11 @@ class Engine:
         self._check(self.L.tcmp_ik(self.h, _d(poses), _d(free_q7), len(poses), _d(sols),
                                    cnt.ctypes.data_as(_i32p)))
         return sols, cnt
+
+    def debug_counters(self, n=8):
+        out = (ctypes.c_uint64 * n)()
+        self._check(self.L.tcmp_debug_counters(self.h, out, n))
+        return list(out)
 
     def fk(self, q):
         """ikfast get_fk: q (n, 7) -> (n, 12) rows (rotation row-major, position)."""

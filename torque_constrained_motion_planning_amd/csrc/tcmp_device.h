@@ -77,13 +77,60 @@ struct Geo {
   const double* __restrict__ verts;   // [V][4]
   const double* __restrict__ planes;  // [F][8] n(3) dmax wmin
   const double* __restrict__ edges;   // [E][16] e | va | n1 | n2
+  // fp32 copy for the first pass of the exact test (kernels stage it in LDS)
+  const float* __restrict__ verts32;    // [V][3]
+  const float4* __restrict__ planes32;  // [F]: n, dmax
+  const ushort4* __restrict__ eidx;     // [E]: va vb (vertex rows) f1 f2 (plane rows)
 };
+__host__ __device__ constexpr unsigned geo_lds_bytes() {
+  return TCMP_TOTAL_PLANES * 16u + TCMP_TOTAL_VERTS * 12u + TCMP_TOTAL_EDGES * 8u;
+}
 
 // obstacle record on device: c(3) B(9 row-major, columns = axes) h(3) aligned(1) pad -> 16
 struct Scene {
-  const double* __restrict__ obs;  // [n][16]
+  const double* __restrict__ obs;    // [n][16]
   int n_obs;
+  const float* __restrict__ obs32;   // [n][8]: world-AABB centre(3), H - kPen + margin (3)
+  unsigned* wq;                      // this wave's LDS pair queue (collides_wave), kQcap + 2
 };
+constexpr int kQcap = 128;           // queued (lane, link, obstacle) pairs per wave
+constexpr unsigned kQwaveBytes = (kQcap + 2) * 4;
+
+// Obstacle records and the fp32 hull geometry are staged in LDS by every kernel that runs
+// collision checks (dynamic shared memory, stage_lds_bytes(n) per block): the per-(link,
+// obstacle) loop then reads LDS broadcasts instead of waiting on a global load per obstacle,
+// and the exact test's gathers hit LDS.  Layout: o64 [n][16] f64 | o32 [n][8] f32 |
+// planes32 [F] float4 | verts32 [V][3] | eidx [E] ushort4.
+constexpr int kMaxObstacles = 384;
+__host__ __device__ constexpr unsigned scene_lds_bytes(int n_obs) {
+  return (unsigned)(n_obs > 0 ? n_obs : 1) * (16 * sizeof(double) + 8 * sizeof(float));
+}
+__host__ __device__ constexpr unsigned stage_lds_bytes(int n_obs) {
+  return scene_lds_bytes(n_obs) + geo_lds_bytes() + 4 * kQwaveBytes;  // 256-thread blocks
+}
+__device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* lds, Scene& so,
+                                          Geo& go) {
+  const int n = sc.n_obs > 0 ? sc.n_obs : 1;
+  double* o64 = lds;
+  float* o32 = reinterpret_cast<float*>(lds + 16 * n);
+  float4* pl = reinterpret_cast<float4*>(o32 + 8 * n);
+  float* vt = reinterpret_cast<float*>(pl + TCMP_TOTAL_PLANES);
+  uint2* ei = reinterpret_cast<uint2*>(vt + 3 * TCMP_TOTAL_VERTS);
+  unsigned* wq = reinterpret_cast<unsigned*>(ei + TCMP_TOTAL_EDGES) +
+                 (threadIdx.x >> 6) * (kQwaveBytes / 4);
+  for (int i = threadIdx.x; i < sc.n_obs * 16; i += blockDim.x) o64[i] = sc.obs[i];
+  for (int i = threadIdx.x; i < sc.n_obs * 8; i += blockDim.x) o32[i] = sc.obs32[i];
+  for (int i = threadIdx.x; i < TCMP_TOTAL_PLANES; i += blockDim.x) pl[i] = g.planes32[i];
+  for (int i = threadIdx.x; i < 3 * TCMP_TOTAL_VERTS; i += blockDim.x) vt[i] = g.verts32[i];
+  const uint2* gei = reinterpret_cast<const uint2*>(g.eidx);
+  for (int i = threadIdx.x; i < TCMP_TOTAL_EDGES; i += blockDim.x) ei[i] = gei[i];
+  __syncthreads();
+  so = Scene{o64, sc.n_obs, o32, wq};
+  go = g;
+  go.planes32 = pl;
+  go.verts32 = vt;
+  go.eidx = reinterpret_cast<const ushort4*>(ei);
+}
 
 struct TorqueCfg {
   int mode;      // 0 base, 1 nov, 2 rne
@@ -301,15 +348,49 @@ __device__ __forceinline__ bool torque_ok(const double cq[7], const double sq[7]
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
+// Wave reductions: two quad_perm and two row_ror DPP steps reduce each 16-lane row inside
+// the VALU, then four readlanes combine the rows -- no LDS round trips (ds_bpermute).  The
+// result is wave-uniform.  Call with every lane of the wave active.
+template <int C>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, true);
+}
+template <int C>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(dpp_i<C>(__float_as_int(v)));
+}
+template <int C>
+__device__ __forceinline__ double dpp_d(double v) {
+  return __hiloint2double(dpp_i<C>(__double2hiint(v)), dpp_i<C>(__double2loint(v)));
+}
+__device__ __forceinline__ float readlane_f(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 __device__ __forceinline__ double wave_min(double x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = fmin(x, __shfl_xor(x, o));
-  return x;
+  x = fmin(x, dpp_d<0xB1>(x));
+  x = fmin(x, dpp_d<0x4E>(x));
+  x = fmin(x, dpp_d<0x124>(x));
+  x = fmin(x, dpp_d<0x128>(x));
+  return fmin(fmin(readlane_d(x, 0), readlane_d(x, 16)), fmin(readlane_d(x, 32), readlane_d(x, 48)));
 }
 __device__ __forceinline__ double wave_max(double x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = fmax(x, __shfl_xor(x, o));
-  return x;
+  x = fmax(x, dpp_d<0xB1>(x));
+  x = fmax(x, dpp_d<0x4E>(x));
+  x = fmax(x, dpp_d<0x124>(x));
+  x = fmax(x, dpp_d<0x128>(x));
+  return fmax(fmax(readlane_d(x, 0), readlane_d(x, 16)), fmax(readlane_d(x, 32), readlane_d(x, 48)));
+}
+__device__ __forceinline__ int wave_min_int(int x) {
+  x = min(x, dpp_i<0xB1>(x));
+  x = min(x, dpp_i<0x4E>(x));
+  x = min(x, dpp_i<0x124>(x));
+  x = min(x, dpp_i<0x128>(x));
+  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
+             min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -413,6 +494,137 @@ __device__ __noinline__ double exact_pd_wave(int link, const Pose pose,
   return fmin(pd, wave_min(loc));
 }
 
+__device__ __forceinline__ float wave_minf(float x) {
+  x = fminf(x, dpp_f<0xB1>(x));
+  x = fminf(x, dpp_f<0x4E>(x));
+  x = fminf(x, dpp_f<0x124>(x));
+  x = fminf(x, dpp_f<0x128>(x));
+  return fminf(fminf(readlane_f(x, 0), readlane_f(x, 16)), fminf(readlane_f(x, 32), readlane_f(x, 48)));
+}
+__device__ __forceinline__ float wave_maxf(float x) {
+  x = fmaxf(x, dpp_f<0xB1>(x));
+  x = fmaxf(x, dpp_f<0x4E>(x));
+  x = fmaxf(x, dpp_f<0x124>(x));
+  x = fmaxf(x, dpp_f<0x128>(x));
+  return fmaxf(fmaxf(readlane_f(x, 0), readlane_f(x, 16)), fmaxf(readlane_f(x, 32), readlane_f(x, 48)));
+}
+
+// fp32 first pass of exact_pd_wave on the LDS geometry.  Same candidate axes and the same
+// early-out; returns NaN when an axis is too close to degenerate for fp32 to classify it the
+// way fp64 does (silhouette sign, tiny cross product, orientation), so the caller falls back
+// to the fp64 test.  Otherwise |result - fp64 result| is far below kExactGuard (errors of a
+// few 1e-6 m for coordinates of a few metres), and only results within kExactGuard of kPen
+// are re-evaluated in fp64: the collision decision is always the fp64 one.
+constexpr float kExactGuard = 1e-4f;
+#ifdef TCMP_PROF
+// exact32 outcomes: [0] box-face early exit, [1] facets alone below kPen - guard,
+// [2] full evaluation, [3] degenerate (fp64 fallback)
+__device__ unsigned long long g_exact_stats[4];
+#endif
+__device__ __noinline__ float exact_pd_wave32(int link, const Pose pose,
+                                              const double* __restrict__ ob, const Geo g) {
+  const int lane = lane_id();
+  const double* R = pose.R;
+  const double* p = pose.p;
+  const double d[3] = {ob[0] - p[0], ob[1] - p[1], ob[2] - p[2]};
+  float cl[3], A[9];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    cl[i] = (float)(R[0 + i] * d[0] + R[3 + i] * d[1] + R[6 + i] * d[2]);
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      A[3 * i + j] = (float)(R[0 + i] * ob[3 + j] + R[3 + i] * ob[6 + j] + R[6 + i] * ob[9 + j]);
+  }
+  const float h[3] = {(float)ob[12], (float)ob[13], (float)ob[14]};
+  constexpr float P = (float)kPen;
+  const int v0 = tcmp_geo_vert_off[link], v1 = tcmp_geo_vert_off[link + 1];
+  const int f0 = tcmp_geo_plane_off[link], f1 = tcmp_geo_plane_off[link + 1];
+  const int e0 = tcmp_geo_edge_off[link], e1 = tcmp_geo_edge_off[link + 1];
+  float mn0 = INFINITY, mn1 = INFINITY, mn2 = INFINITY;
+  float mx0 = -INFINITY, mx1 = -INFINITY, mx2 = -INFINITY;
+  for (int v = v0 + lane; v < v1; v += 64) {
+    const float x = g.verts32[3 * v], y = g.verts32[3 * v + 1], z = g.verts32[3 * v + 2];
+    const float d0 = A[0] * x + A[3] * y + A[6] * z;
+    const float d1 = A[1] * x + A[4] * y + A[7] * z;
+    const float d2 = A[2] * x + A[5] * y + A[8] * z;
+    mn0 = fminf(mn0, d0); mx0 = fmaxf(mx0, d0);
+    mn1 = fminf(mn1, d1); mx1 = fmaxf(mx1, d1);
+    mn2 = fminf(mn2, d2); mx2 = fmaxf(mx2, d2);
+  }
+  mn0 = wave_minf(mn0); mn1 = wave_minf(mn1); mn2 = wave_minf(mn2);
+  mx0 = wave_maxf(mx0); mx1 = wave_maxf(mx1); mx2 = wave_maxf(mx2);
+  float pd;
+  {
+    const float pc0 = A[0] * cl[0] + A[3] * cl[1] + A[6] * cl[2];
+    const float pc1 = A[1] * cl[0] + A[4] * cl[1] + A[7] * cl[2];
+    const float pc2 = A[2] * cl[0] + A[5] * cl[1] + A[8] * cl[2];
+    pd = fminf(fminf(mx0 - pc0 + h[0], pc0 + h[0] - mn0),
+               fminf(fminf(mx1 - pc1 + h[1], pc1 + h[1] - mn1),
+                     fminf(mx2 - pc2 + h[2], pc2 + h[2] - mn2)));
+  }
+  if (pd < P - kExactGuard) {
+#ifdef TCMP_PROF
+    if (lane == 0) atomicAdd(&g_exact_stats[0], 1ull);
+#endif
+    return pd;
+  }
+  float loc = INFINITY;
+  for (int f = f0 + lane; f < f1; f += 64) {
+    const float4 n = g.planes32[f];
+    const float pc = n.x * cl[0] + n.y * cl[1] + n.z * cl[2];
+    const float rad = h[0] * fabsf(n.x * A[0] + n.y * A[3] + n.z * A[6]) +
+                      h[1] * fabsf(n.x * A[1] + n.y * A[4] + n.z * A[7]) +
+                      h[2] * fabsf(n.x * A[2] + n.y * A[5] + n.z * A[8]);
+    loc = fminf(loc, n.w - pc + rad);
+  }
+#ifdef TCMP_PROF
+  {
+    const float lf = wave_minf(loc);
+    if (lane == 0 && lf < P - kExactGuard) atomicAdd(&g_exact_stats[1], 1ull);
+  }
+#endif
+  bool deg = false;
+  for (int e = e0 + lane; e < e1; e += 64) {
+    const ushort4 ix = g.eidx[e];
+    const float ax0 = g.verts32[3 * ix.x], ay0 = g.verts32[3 * ix.x + 1], az0 = g.verts32[3 * ix.x + 2];
+    const float ex = g.verts32[3 * ix.y] - ax0, ey = g.verts32[3 * ix.y + 1] - ay0,
+                ez = g.verts32[3 * ix.y + 2] - az0;
+    const float4 n1 = g.planes32[ix.z];
+    const float4 n2 = g.planes32[ix.w];
+    const float el2 = ex * ex + ey * ey + ez * ez;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const float a0 = A[0 + i], a1 = A[3 + i], a2 = A[6 + i];
+      const float s1 = n1.x * a0 + n1.y * a1 + n1.z * a2;
+      const float s2 = n2.x * a0 + n2.y * a1 + n2.z * a2;
+      deg |= ((int)(fabsf(s1) < 1e-5f) | (int)(fabsf(s2) < 1e-5f)) != 0;
+      if (s1 * s2 < 0.f) {
+        float m0 = ey * a2 - ez * a1, m1 = ez * a0 - ex * a2, m2 = ex * a1 - ey * a0;
+        const float len2 = m0 * m0 + m1 * m1 + m2 * m2;
+        if (len2 < 1e-8f * el2) {
+          deg = true;
+        } else {
+          const float ori = m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z);
+          const float il = rsqrtf(len2);
+          deg |= fabsf(ori) * il < 1e-4f;
+          if (ori < 0.f) { m0 = -m0; m1 = -m1; m2 = -m2; }
+          const float hv = m0 * ax0 + m1 * ay0 + m2 * az0;
+          const float pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
+          const float rad = h[0] * fabsf(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
+                            h[1] * fabsf(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
+                            h[2] * fabsf(m0 * A[2] + m1 * A[5] + m2 * A[8]);
+          loc = fminf(loc, (hv - pc + rad) * il);
+        }
+      }
+    }
+  }
+#ifdef TCMP_PROF
+  if (lane == 0) atomicAdd(&g_exact_stats[__ballot(deg) ? 3 : 2], 1ull);
+#endif
+  if (__ballot(deg)) return __builtin_nanf("");
+  return fminf(pd, wave_minf(loc));
+}
+
 // ------------------------------------------------------------------------------------------
 // configuration check: collision (limits + 10 links x obstacles) and torque test.
 // MUST be called by every lane of the wave (uniform control flow); `active` masks lanes.
@@ -425,6 +637,10 @@ struct StepStats {
   unsigned pairs_tested;  // tier-1 tests
   unsigned pairs_sat;     // tier-2/3 evaluations
   unsigned pairs_exact;   // tier-4 evaluations (wave-level count, lane 0)
+#ifdef TCMP_PROF
+  unsigned long long cyc_exact = 0;  // shader clocks spent in tier 4 (profiling builds)
+  unsigned long long cyc_t123 = 0;   // ... in tiers 1-3 (maybe branch, excluding tier 4)
+#endif
 };
 
 __device__ __forceinline__ void frame_step(double R[9], double p[3], const double Rl[9],
@@ -454,7 +670,6 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
   const bool aligned = ob[15] != 0.0;
   // tier 1: link OBB extent along the obstacle axes
   double dc[3] = {wc[0] - ob[0], wc[1] - ob[1], wc[2] - ob[2]};
-  st.pairs_tested++;
   if (aligned) {
     if ((h0 + aabb[0]) - fabs(dc[0]) < kPen) return 0;
     if ((h1 + aabb[1]) - fabs(dc[1]) < kPen) return 0;
@@ -527,10 +742,28 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
   return inner_all ? 1 : 2;
 }
 
-// world frames of the 10 collision links are generated incrementally; `fn(link, R, p)` is
-// invoked in link order with uniform control flow.
-template <typename F>
-__device__ __forceinline__ void for_each_link_frame(const double cq[7], const double sq[7], F&& fn) {
+// Returns collision flag; all lanes must call.  `active` lanes only contribute.
+//
+// Phase A (every step): the link frames are generated in a runtime loop over the 10 links and
+// each link's world AABB is tested against each obstacle's world AABB in fp32 (tier 0,
+// branch-free; "maybe" iff the overlap could reach kPen on all three axes -- AABBs contain
+// the shapes, so a penetration >= kPen always gives a "maybe").  Maybe pairs are queued in
+// this wave's LDS queue as (lane, link, obstacle).
+// Phase B (flush, when the queue could overflow and at the end): the queued pairs are
+// processed lane-parallel -- each lane rebuilds its pair's link pose in fp64 from the owning
+// lane's cos/sin and runs tiers 1-3 (classify_pair) -- and the undecided ones go through the
+// wave-cooperative exact test (fp32 first pass, fp64 when near kPen or degenerate).
+// Tiers 0-3 are conservative bounds of the exact test, so the answer is the exact test's.
+__device__ __forceinline__ double sel7(const double v[7], int j) {
+  double r = v[0];
+#pragma unroll
+  for (int k = 1; k < 7; ++k) r = (j == k) ? v[k] : r;
+  return r;
+}
+
+// world frame of `link` (0..9) as collides_wave's phase A builds it, for per-lane links
+__device__ __forceinline__ void link_pose(int link, const double cq[7], const double sq[7],
+                                          double Ro[9], double po[3]) {
   double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
@@ -538,73 +771,180 @@ __device__ __forceinline__ void for_each_link_frame(const double cq[7], const do
     const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
     const double t[3] = {kJx[j], kJy[j], kJz[j]};
     frame_step(R, p, Rl, t);
-    fn(j, R, p);
-  }
-  {
-    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const double tz[3] = {0, 0, kFlangeZ};
-    frame_step(R, p, I, tz);
-    const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
-    const double z0[3] = {0, 0, 0};
-    frame_step(R, p, Rz, z0);
-    fn(7, R, p);
-    double Rf[9], pf[3];
+    if (j == link) {
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Rf[k] = R[k];
-    const double tl[3] = {0, kFingerOpen, kFingerZ};
-    pf[0] = p[0]; pf[1] = p[1]; pf[2] = p[2];
-    frame_step(Rf, pf, I, tl);
-    fn(8, Rf, pf);
-    const double tr[3] = {0, -kFingerOpen, kFingerZ};
-    frame_step(R, p, I, tr);
-    fn(9, R, p);
+      for (int k = 0; k < 9; ++k) Ro[k] = R[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) po[k] = p[k];
+    }
+  }
+  const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+  const double tz[3] = {0, 0, kFlangeZ};
+  frame_step(R, p, I, tz);
+  const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
+  const double z0[3] = {0, 0, 0};
+  frame_step(R, p, Rz, z0);
+  if (link >= 7) {
+    const double tf[3] = {0, link == 8 ? kFingerOpen : -kFingerOpen, kFingerZ};
+    if (link > 7) frame_step(R, p, I, tf);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) Ro[k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) po[k] = p[k];
   }
 }
 
-// Returns collision flag; all lanes must call.  `active` lanes only contribute.
+__device__ __forceinline__ void link_obb(int link, const double R[9], const double p[3],
+                                         double wc[3], double U[9], double aabb[3]) {
+  const double* bx = tcmp_geo_boxes + 18 * link;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    wc[i] = R[3 * i + 0] * bx[0] + R[3 * i + 1] * bx[1] + R[3 * i + 2] * bx[2] + p[i];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      U[3 * i + j] = R[3 * i + 0] * bx[3 + j] + R[3 * i + 1] * bx[6 + j] + R[3 * i + 2] * bx[9 + j];
+  }
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
+}
+
 __device__ __forceinline__ bool collides_wave(const double q[7], const double cq[7],
                                               const double sq[7], bool active,
                                               const Scene sc, const Geo g, StepStats& st) {
   bool coll = active && limits_violated(q);
   if (sc.n_obs == 0) return coll;
   const int lane = lane_id();
-  for_each_link_frame(cq, sq, [&](int link, const double R[9], const double p[3]) {
-    // stop once no active lane is still free (uniform test)
-    if (__ballot(active && !coll) == 0) return;
-    const double* bx = tcmp_geo_boxes + 18 * link;
-    double wc[3], U[9], aabb[3];
+  unsigned* queue = sc.wq;
+  unsigned long long* cmask = reinterpret_cast<unsigned long long*>(sc.wq + kQcap);
+  if (lane == 0) *cmask = 0ull;
+  __builtin_amdgcn_wave_barrier();
+  int count = 0;  // wave-uniform
+  const bool live = active && !coll;
+  // ---- phase B ------------------------------------------------------------------------
+  auto flush = [&]() {
+    __builtin_amdgcn_wave_barrier();
+#ifdef TCMP_PROF
+    const unsigned long long tf0 = clock64();
+#endif
+    for (int b = 0; b < count; b += 64) {
+      const bool has = b + lane < count;
+      const unsigned ent = has ? queue[b + lane] : 0u;
+      const int src = (int)(ent & 63u), lk = (int)((ent >> 6) & 15u), o = (int)(ent >> 10);
+      double c[7], s[7];
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      wc[i] = R[3 * i + 0] * bx[0] + R[3 * i + 1] * bx[1] + R[3 * i + 2] * bx[2] + p[i];
-#pragma unroll
-      for (int j = 0; j < 3; ++j)
-        U[3 * i + j] = R[3 * i + 0] * bx[3 + j] + R[3 * i + 1] * bx[6 + j] + R[3 * i + 2] * bx[9 + j];
-    }
-#pragma unroll
-    for (int i = 0; i < 3; ++i)
-      aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
-    for (int o = 0; o < sc.n_obs; ++o) {
-      const double* __restrict__ ob = sc.obs + 16 * o;
+      for (int k = 0; k < 7; ++k) {
+        c[k] = __shfl(cq[k], src);
+        s[k] = __shfl(sq[k], src);
+      }
+      double R[9], p[3];
+      link_pose(lk, c, s, R, p);
       int cls = 0;
-      if (active && !coll) cls = classify_pair(link, R, p, wc, U, aabb, ob, st);
-      coll |= (cls == 1);
+      if (has) {
+        double wc[3], U[9], aabb[3];
+        link_obb(lk, R, p, wc, U, aabb);
+        cls = classify_pair(lk, R, p, wc, U, aabb, sc.obs + 16 * o, st);
+      }
+      if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
       while (pend) {
         const int L = __builtin_ctzll(pend);
+        pend &= pend - 1;
+        const int sL = __shfl(src, L);
+        __builtin_amdgcn_wave_barrier();
+        if ((*cmask >> sL) & 1ull) continue;  // that lane already collides
+        const int lL = __shfl(lk, L), oL = __shfl(o, L);
         Pose PL;
 #pragma unroll
         for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
 #pragma unroll
         for (int k = 0; k < 3; ++k) PL.p[k] = __shfl(p[k], L);
-        const double pd = exact_pd_wave(link, PL, ob, g);
-        if (lane == L) {
-          coll |= (pd >= kPen);
+        const double* ob = sc.obs + 16 * oL;
+#ifdef TCMP_PROF
+        const unsigned long long te0 = clock64();
+#endif
+        const float pd32 = exact_pd_wave32(lL, PL, ob, g);
+        const double pd = (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard)
+                              ? (double)pd32
+                              : exact_pd_wave(lL, PL, ob, g);
+#ifdef TCMP_PROF
+        st.cyc_exact += clock64() - te0;
+#endif
+        if (lane == 0) {
           st.pairs_exact++;
+          if (pd >= kPen) atomicOr(cmask, 1ull << sL);
         }
-        pend &= pend - 1;
       }
     }
-  });
+    __builtin_amdgcn_wave_barrier();
+    count = 0;
+#ifdef TCMP_PROF
+    st.cyc_t123 += clock64() - tf0;
+#endif
+  };
+  // ---- phase A ------------------------------------------------------------------------
+  if (live) st.pairs_tested += 10u * (unsigned)sc.n_obs;
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+  double Rh[9], ph[3];
+  for (int link = 0; link < 10; ++link) {  // uniform runtime loop: one copy of the body
+    if (link < 7) {
+      const double cr = kJcr[link], sr = kJsr[link], c = sel7(cq, link), s = sel7(sq, link);
+      const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+      const double t[3] = {kJx[link], kJy[link], kJz[link]};
+      frame_step(R, p, Rl, t);
+    } else if (link == 7) {
+      const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+      const double tz[3] = {0, 0, kFlangeZ};
+      frame_step(R, p, I, tz);
+      const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
+      const double z0[3] = {0, 0, 0};
+      frame_step(R, p, Rz, z0);
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Rh[k] = R[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) ph[k] = p[k];
+    } else {
+      const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+      const double tf[3] = {0, link == 8 ? kFingerOpen : -kFingerOpen, kFingerZ};
+#pragma unroll
+      for (int k = 0; k < 9; ++k) R[k] = Rh[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) p[k] = ph[k];
+      frame_step(R, p, I, tf);
+    }
+    double wc[3], U[9], aabb[3];
+    link_obb(link, R, p, wc, U, aabb);
+    const float wx = (float)wc[0], wy = (float)wc[1], wz = (float)wc[2];
+    const float ax = (float)aabb[0] + 1e-5f, ay = (float)aabb[1] + 1e-5f, az = (float)aabb[2] + 1e-5f;
+    for (int o0 = 0; o0 < sc.n_obs; o0 += 4) {
+      // four obstacles per pass: all LDS reads issued before the first compare
+      unsigned mb = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int o = min(o0 + u, sc.n_obs - 1);
+        const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
+        const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
+        const bool m = ((int)(o0 + u < sc.n_obs) & (int)live & (int)(fabsf(wx - oa.x) <= ax + ob4.x) &
+                        (int)(fabsf(wy - oa.y) <= ay + ob4.y) &
+                        (int)(fabsf(wz - oa.z) <= az + ob4.z)) != 0;
+        mb |= (unsigned)m << u;
+      }
+      if (__ballot(mb != 0u) == 0) continue;
+#pragma unroll 1
+      for (int u = 0; u < 4; ++u) {
+        const bool m = (mb >> u) & 1u;
+        const uint64_t bm = __ballot(m);
+        if (bm == 0) continue;
+        if (count + 64 > kQcap) flush();
+        if (m) queue[count + (int)__popcll(bm & ((1ull << lane) - 1ull))] =
+            (unsigned)lane | ((unsigned)link << 6) | ((unsigned)(o0 + u) << 10);
+        count += (int)__popcll(bm);
+      }
+    }
+  }
+  if (count) flush();
+  __builtin_amdgcn_wave_barrier();
+  coll |= active && ((*cmask >> lane) & 1ull);
   return coll;
 }
 

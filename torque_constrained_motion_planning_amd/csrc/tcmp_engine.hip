@@ -68,6 +68,7 @@ struct DevState {
   int status;
   int overflow;
   int nn_queue[8];       // per-XCD work queues of k_nearest_wave32
+  unsigned long long prof[16];  // TCMP_PROF builds: k_edges clock breakdown + exact-test stats
 };
 
 struct PlanParams {
@@ -466,20 +467,31 @@ struct EdgeJob {
 #ifndef TCMP_EDGE_MINW
 #define TCMP_EDGE_MINW 2  // min waves per SIMD the register allocation must allow
 #endif
-__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanParams P, Scene sc, Geo g,
+__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanParams P, Scene sc_g, Geo g_g,
                                                DevState* st) {
+  extern __shared__ double tcmp_lds[];
+  Scene sc;
+  Geo g;
+  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
   const int lane = lane_id();
   int e = -1, i = 0, n = 0;
   bool done = false;
   double q[7], q2[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) { q[k] = 0.5 * (kLo[k] + kHi[k]); q2[k] = q[k]; }
-  StepStats ss = {0, 0, 0};
+  StepStats ss = {};
   unsigned long long steps = 0;
+#ifdef TCMP_PROF
+  unsigned long long c_total = 0, c_fetch = 0, c_coll = 0, c_torque = 0, c_tail = 0, c_sincos = 0;
+  const unsigned long long c_start = clock64();
+#endif
   double res[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) res[k] = P.res[k];
   while (true) {
+#ifdef TCMP_PROF
+    unsigned long long c0 = clock64();
+#endif
     const bool need = !done && e < 0;
     const uint64_t m = __ballot(need);
     if (m) {
@@ -502,6 +514,9 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
       }
     }
     if (__ballot(!done) == 0) break;
+#ifdef TCMP_PROF
+    { const unsigned long long c1 = clock64(); c_fetch += c1 - c0; c0 = c1; }
+#endif
     const bool active = e >= 0;
     double qn[7];
 #pragma unroll
@@ -510,12 +525,21 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     double cq[7], sq[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
+#ifdef TCMP_PROF
+    { const unsigned long long c1 = clock64(); c_sincos += c1 - c0; c0 = c1; }
+#endif
     const bool coll = collides_wave(qn, cq, sq, active, sc, g, ss);
+#ifdef TCMP_PROF
+    { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
+#endif
     bool ok = active && !coll;
     if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
       const double z[7] = {0, 0, 0, 0, 0, 0, 0};
       ok = torque_ok<false>(cq, sq, z, z, P.mass);
     }
+#ifdef TCMP_PROF
+    { const unsigned long long c1 = clock64(); c_torque += c1 - c0; c0 = c1; }
+#endif
     if (active) {
       ++steps;
       if (ok) {
@@ -530,6 +554,9 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
         e = -1;
       }
     }
+#ifdef TCMP_PROF
+    c_tail += clock64() - c0;
+#endif
   }
   const unsigned long long a = wave_sum_u64(steps), b = wave_sum_u64(ss.pairs_tested),
                            c = wave_sum_u64(ss.pairs_sat), d = wave_sum_u64(ss.pairs_exact);
@@ -538,6 +565,17 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     atomicAdd(&st->pairs_tested, b);
     atomicAdd(&st->pairs_sat, c);
     atomicAdd(&st->pairs_exact, d);
+#ifdef TCMP_PROF
+    c_total = clock64() - c_start;
+    atomicAdd(&st->prof[0], c_total);
+    atomicAdd(&st->prof[1], c_fetch);
+    atomicAdd(&st->prof[2], c_coll);
+    atomicAdd(&st->prof[3], c_torque);
+    atomicAdd(&st->prof[4], c_tail);
+    atomicAdd(&st->prof[5], ss.cyc_exact);
+    atomicAdd(&st->prof[6], c_sincos);
+    atomicAdd(&st->prof[7], ss.cyc_t123);
+#endif
   }
 }
 
@@ -676,7 +714,11 @@ __global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st,
 
 __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st, Tree tr,
                                                       const int* rwlist, const int* nbr,
-                                                      const int* ncount, Scene sc, Geo g) {
+                                                      const int* ncount, Scene sc_g, Geo g_g) {
+  extern __shared__ double tcmp_lds[];
+  Scene sc;
+  Geo g;
+  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
   const long long R = st->rw_count, T = st->snap;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = t < R && ncount[t] > 0;
@@ -933,8 +975,12 @@ __global__ void k_traj_post(DevState* st) {
 // ------------------------------------------------------------------------------------------
 // utility kernels behind the batched C-ABI entry points
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_check_configs(const double* q, long long n, Scene sc,
-                                                       Geo g, int* collides) {
+__global__ __launch_bounds__(256) void k_check_configs(const double* q, long long n, Scene sc_g,
+                                                       Geo g_g, int* collides) {
+  extern __shared__ double tcmp_lds[];
+  Scene sc;
+  Geo g;
+  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < n;
   double x[7];
@@ -1041,6 +1087,9 @@ struct tcmp_handle {
   int cu_count = 0;
   DBuf<double> verts, planes, edges;
   DBuf<double> obs;
+  DBuf<float> obs32;
+  DBuf<float> verts32, planes32;
+  DBuf<unsigned short> eidx;
   int n_obs = 0;
   DevState* st = nullptr;
   // plan
@@ -1064,7 +1113,7 @@ struct tcmp_handle {
   DBuf<int> chome, bcount, boff;
   DBuf<unsigned char> sort_tmp;
   bool nn_brute = false;
-  int nn_waves_per_cu = 24;
+  int nn_waves_per_cu = 16;
   DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
@@ -1080,8 +1129,12 @@ struct tcmp_handle {
   long long launches_nearest = 0;
   int edge_blocks = 0;
 
-  Geo geo() const { return Geo{verts.p, planes.p, edges.p}; }
-  Scene scene() const { return Scene{obs.p, n_obs}; }
+  Geo geo() const {
+    return Geo{verts.p, planes.p, edges.p, verts32.p,
+               reinterpret_cast<const float4*>(planes32.p),
+               reinterpret_cast<const ushort4*>(eidx.p)};
+  }
+  Scene scene() const { return Scene{obs.p, n_obs, obs32.p}; }
 
   hipEvent_t get_event() {
     if (!ev_pool.empty()) {
@@ -1229,7 +1282,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(k_edges, dim3((unsigned)blocks), dim3(256), 0, h->stream, J, P,
+  hipLaunchKernelGGL(k_edges, dim3((unsigned)blocks), dim3(256), stage_lds_bytes(h->n_obs), h->stream, J, P,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1259,6 +1312,21 @@ extern "C" {
 const char* tcmp_last_error(void) { return g_err.c_str(); }
 int tcmp_version(void) { return 1; }
 
+int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
+  if (int rc = set_dev(h)) return rc;
+  if (!out || n < 0 || n > 16) return fail(-1, "bad arguments");
+  DevState s;
+  HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  for (int i = 0; i < n; ++i) out[i] = s.prof[i];
+#ifdef TCMP_PROF
+  unsigned long long ex[4];
+  HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
+  for (int i = 0; i < 4 && 8 + i < n; ++i) out[8 + i] = ex[i];
+#endif
+  return 0;
+}
+
 int tcmp_device_count(int* n) {
   if (!n) return fail(-1, "null");
   HIPCHK(hipGetDeviceCount(n));
@@ -1285,6 +1353,26 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMemcpy(h->verts.p, tcmp_geo_verts, sizeof(tcmp_geo_verts), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->planes.p, tcmp_geo_planes, sizeof(tcmp_geo_planes), hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(h->edges.p, tcmp_geo_edges, sizeof(tcmp_geo_edges), hipMemcpyHostToDevice));
+  {
+    // fp32 geometry for the exact test's first pass (staged in LDS by the kernels)
+    std::vector<float> v32(3 * TCMP_TOTAL_VERTS), p32(4 * TCMP_TOTAL_PLANES);
+    for (int v = 0; v < TCMP_TOTAL_VERTS; ++v)
+      for (int k = 0; k < 3; ++k) v32[3 * v + k] = (float)tcmp_geo_verts[4 * v + k];
+    for (int f = 0; f < TCMP_TOTAL_PLANES; ++f)
+      for (int k = 0; k < 4; ++k) p32[4 * f + k] = (float)tcmp_geo_planes[8 * f + k];
+    rc = h->verts32.ensure(v32.size());
+    rc = rc ? rc : h->planes32.ensure(p32.size());
+    rc = rc ? rc : h->eidx.ensure(4 * TCMP_TOTAL_EDGES);
+    if (rc) { delete h; return rc; }
+    HIPCHK(hipMemcpy(h->verts32.p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->planes32.p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(h->eidx.p, tcmp_geo_edge_idx, sizeof(tcmp_geo_edge_idx), hipMemcpyHostToDevice));
+    // dynamic LDS above 64 KiB per workgroup must be allowed explicitly
+    const int lim = (int)stage_lds_bytes(kMaxObstacles);
+    HIPCHK(hipFuncSetAttribute((const void*)k_edges, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    HIPCHK(hipFuncSetAttribute((const void*)k_check_configs, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    HIPCHK(hipFuncSetAttribute((const void*)k_rewire_apply, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+  }
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
   const char* nb_env = getenv("TCMP_NN_BRUTE");
@@ -1299,6 +1387,10 @@ int tcmp_destroy(tcmp_handle* h) {
   if (!h) return 0;
   (void)hipSetDevice(h->device);
   (void)hipStreamSynchronize(h->stream);
+  h->verts32.release();
+  h->planes32.release();
+  h->eidx.release();
+  h->obs32.release();
   for (auto* b : {&h->verts, &h->planes, &h->edges, &h->obs, &h->cfg, &h->tgt, &h->cand,
                   &h->last, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
                   &h->s1, &h->s2, &h->s3})
@@ -1338,6 +1430,9 @@ int tcmp_destroy(tcmp_handle* h) {
 int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
   if (int rc = set_dev(h)) return rc;
   if (n_obs < 0 || (n_obs > 0 && !obb)) return fail(-1, "bad obstacle array");
+  if (n_obs > kMaxObstacles)
+    return fail(-1, "too many obstacles (" + std::to_string(n_obs) + " > " +
+                        std::to_string(kMaxObstacles) + ", the LDS-staged scene limit)");
   std::vector<double> tmp((size_t)std::max(n_obs, 1) * 16, 0.0);
   for (int o = 0; o < n_obs; ++o) {
     const double* s = obb + 15 * o;
@@ -1350,8 +1445,23 @@ int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
     d[15] = aligned ? 1.0 : 0.0;
     if (!(s[12] >= 0 && s[13] >= 0 && s[14] >= 0)) return fail(-1, "negative half extent");
   }
+  // tier-0 records: world AABB centre and (half extent - kPen + margin), fp32 rounded outward
+  std::vector<float> t32((size_t)std::max(n_obs, 1) * 8, 0.f);
+  for (int o = 0; o < n_obs; ++o) {
+    const double* d = tmp.data() + 16 * o;
+    float* f = t32.data() + 8 * o;
+    for (int i = 0; i < 3; ++i) {
+      const double H = fabs(d[3 + 3 * i]) * d[12] + fabs(d[4 + 3 * i]) * d[13] +
+                       fabs(d[5 + 3 * i]) * d[14];
+      f[i] = (float)d[i];
+      f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(d[i]) + H));
+    }
+  }
   if (int rc = h->obs.ensure(tmp.size())) return rc;
+  if (int rc = h->obs32.ensure(t32.size())) return rc;
   HIPCHK(hipMemcpyAsync(h->obs.p, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice,
+                        h->stream));
+  HIPCHK(hipMemcpyAsync(h->obs32.p, t32.data(), t32.size() * sizeof(float), hipMemcpyHostToDevice,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->n_obs = n_obs;
@@ -1448,7 +1558,7 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   int rc = upload7(h, h->s0, q, n);
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_check_configs, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->s0.p,
+  hipLaunchKernelGGL(k_check_configs, dim3(grid_for(n, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, h->s0.p,
                      (long long)n, h->scene(), h->geo(), h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
@@ -1731,7 +1841,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_rewire_apply, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+  hipLaunchKernelGGL(k_rewire_apply, dim3(grid_for(nb, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);

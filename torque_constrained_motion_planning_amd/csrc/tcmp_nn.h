@@ -124,11 +124,6 @@ __device__ __forceinline__ double box_lb(const float* b, const double s[7], cons
   return lb;
 }
 
-__device__ __forceinline__ int wave_min_int(int x) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) x = min(x, __shfl_xor(x, o));
-  return x;
-}
 
 // position p of the zig-zag walk out from h over [0, n): h, h+1, h-1, h+2, h-2, ...;
 // once one side is exhausted the walk continues on the other.  -1 if p >= n.

@@ -32,8 +32,31 @@ __device__ __forceinline__ unsigned xcc_id() {
   return x & 7u;
 }
 
+// Lower bound of the weighted squared distance from s to a float box, in fp32, never above
+// the fp64 value box_lb<UW> would give: each gap is shrunk by 1e-6 (> the fp32 rounding of
+// s and of the subtraction for |q| <= kNnCoordMax) and the sum by 1e-6 relative.
 template <bool UW>
-__global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* st,
+__device__ __forceinline__ float box_lb32(const float* b, const float s[7], const float w[7]) {
+  const float4 l0 = *reinterpret_cast<const float4*>(b);
+  const float4 l1 = *reinterpret_cast<const float4*>(b + 4);
+  const float4 h0 = *reinterpret_cast<const float4*>(b + 8);
+  const float4 h1 = *reinterpret_cast<const float4*>(b + 12);
+  const float lo[7] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z};
+  const float hi[7] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z};
+  float lb = 0.f;
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    const float g = fmaxf(0.f, fmaxf(lo[k] - s[k], s[k] - hi[k]) - 1e-6f);
+    lb = fmaf(UW ? g : w[k] * g, g, lb);
+  }
+  return lb * 0.999999f;
+}
+
+#ifndef TCMP_NN_MINB
+#define TCMP_NN_MINB 1  // min 256-thread blocks per CU the register allocation must allow
+#endif
+template <bool UW>
+__global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams P, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
                                                         const float* sbox, const double* cand,
@@ -52,6 +75,8 @@ __global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* 
   }
   const double E = kNnE * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
+  const float E32 = __double2float_ru(E * (1.0 + 1e-9)), ru32 = __double2float_ru(ru);
+  const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
   unsigned long long pairs = 0, tests = 0;
   int qi = (int)xcc_id(), tried = 0;
   while (true) {
@@ -122,15 +147,17 @@ __global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* 
       if (r <= Rf) refine(n);
       else r2 = fminf(r2, r);
     };
-    // refresh the pruning threshold and the refine threshold from the exact best
+    // refresh the pruning threshold and the refine threshold from the exact best m, in fp32
+    // rounded upward (m32 >= m, so both thresholds only grow: pruning and refinement stay
+    // conservative)
     auto refresh = [&]() {
-      const double m = wave_min(b1);
-      const double sm = sqrt(m);
-      const double t = sm + ru;
-      const double R = (1.0 + kNnG) * (sm * (1.0 + 1e-12) + E) * (sm * (1.0 + 1e-12) + E) *
-                       (1.0 + 1e-7);
-      Rf = __double2float_ru(R);
-      return t * t * (1.0 + 1e-9) + 1e-300;
+      // (each round-to-nearest step is covered by a 1e-6 relative margin, >> 2^-24)
+      const float m32 = wave_minf(__double2float_ru(b1));
+      const float sm = sqrtf(m32) * 1.000001f;
+      const float t = (sm + ru32) * 1.000001f;
+      const float tr = (sm + E32) * 1.000001f;
+      Rf = tr * tr * kRfac;
+      return t * t * 1.000003f;
     };
     auto scan4 = [&](int c0, int c1, int c2, int c3) {
       const int cs[4] = {c0, c1, c2, c3};
@@ -151,7 +178,7 @@ __global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* 
         if (val[u]) upd(A[u], Bq[u], (long long)cs[u] * kNnC + lane);
       return refresh();
     };
-    double thr;
+    float thr;
     {
       // home chunk: R = inf, every node exact
       const long long n = (long long)hc * kNnC + lane;
@@ -161,17 +188,17 @@ __global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* 
     }
     for (int g = 0; g < nsup; g += 64) {
       const int sidx = zigzag(hs, g + lane, nsup);
-      const double lbs = sidx >= 0 ? box_lb<UW>(sbox + 16 * (size_t)sidx, s, w) : INFINITY;
+      const float lbs = sidx >= 0 ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32) : INFINITY;
       tests += (unsigned long long)min(64, nsup - g);
       uint64_t smask = __ballot(lbs <= thr);
       while (smask) {
         const int i = __builtin_ctzll(smask);
         smask &= smask - 1;
-        if (__shfl(lbs, i) > thr) continue;
-        const int S = __shfl(sidx, i);
+        if (readlane_f(lbs, i) > thr) continue;
+        const int S = __builtin_amdgcn_readlane(sidx, i);
         const int c = S * kNnS + lane;
         const bool cv = c < nch && c != hc;
-        const double lbc = cv ? box_lb<UW>(cbox + 16 * (size_t)c, s, w) : INFINITY;
+        const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32) : INFINITY;
         tests += (unsigned long long)min(kNnS, nch - S * kNnS);
         uint64_t cmask = __ballot(lbc <= thr);
         while (cmask) {
@@ -179,7 +206,7 @@ __global__ __launch_bounds__(256) void k_nearest_wave32(PlanParams P, DevState* 
             while (cmask) {
               const int k = __builtin_ctzll(cmask);
               cmask &= cmask - 1;
-              if (__shfl(lbc, k) <= thr) return S * kNnS + k;
+              if (readlane_f(lbc, k) <= thr) return S * kNnS + k;
             }
             return -1;
           };
