@@ -29,9 +29,9 @@ from torque_constrained_motion_planning_amd import _lib, shard  # noqa: E402
 from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene  # noqa: E402
 
 START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])  # utils.py:45
-PEAK_FP64_TFLOPS = 78.6     # MI355X fp64 vector peak (spec)
+PEAK_FP32_TFLOPS = 157.3    # MI355X fp32 vector peak (spec, MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
-NN_FLOP_PER_PAIR = 21       # 7 sub + 7 fma per (candidate, node) pair (SURVEY 8d F_nn)
+NN_FLOP_PER_PAIR = 21       # 7 sub + 7 fma per (candidate, node) pair, fp32 first pass (SURVEY 8d F_nn)
 NN_BYTES_PER_NODE = 64      # one tree record (q0..q6, cost) streamed per block
 
 
@@ -100,7 +100,7 @@ def main():
     ap.add_argument("--samples", type=int, default=1_000_000)
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--obstacles", type=int, default=16)
-    ap.add_argument("--cpu-samples", type=int, default=20000)
+    ap.add_argument("--cpu-samples", type=int, default=50000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -154,20 +154,21 @@ def main():
         dt = float(t.item())
 
     total_samples = args.samples * args.steps * world
-    # dominant kernel: k_nearest_wave (pruned Morton-chunk fp64 argmin over the snapshot);
-    # ms_nn_scan = hipEvents around its launches only, on the engine's stream
+    # dominant kernel: k_nearest_wave32 (pruned Morton-chunk argmin over the snapshot, fp32
+    # first pass + exact fp64 refinement); ms_nn_scan = hipEvents around its launches only,
+    # on the engine's stream.  Achieved = 21 flop x evaluated pairs / scan time.
     nn_pairs = sum(x["nn_pairs"] for x in results)
     nn_ms = sum(x["ms_nn_scan"] for x in results)
     nn_launches = sum(x["launches_nearest"] for x in results)
     achieved_tflops = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    # HBM traffic per k_nearest launch from the committed rocprofv3 PMC passes of this same
+    # HBM traffic per k_nearest_wave32 launch from the committed rocprofv3 PMC passes of this same
     # workload (profiles/*_pmc_hbm.json; FETCH_SIZE doubled per the gfx950 correction)
     traffic = None
     pmc = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_hbm.json")) \
         if os.path.isdir(os.path.join(REPO, "profiles")) else []
     if pmc:
         d = json.load(open(os.path.join(REPO, "profiles", pmc[-1])))["dispatches"].get(
-            "k_nearest_wave", [])
+            "k_nearest_wave32", [])
         fetch = [x["value_KiB"] for x in d if x["counter"] == "FETCH_SIZE"]
         write = [x["value_KiB"] for x in d if x["counter"] == "WRITE_SIZE"]
         if fetch and len(fetch) == len(write):
@@ -196,13 +197,13 @@ def main():
                    "batch_per_round": args.batch, "execution_time_s": 5.0,
                    "parallelism": "query-sharded x%d" % world},
         "roofline": {
-            "kernel": "k_nearest_wave",
+            "kernel": "k_nearest_wave32",
             "avg_launch_ms": nn_ms / max(1, nn_launches),
-            "bound": "valu_fp64",
+            "bound": "valu_fp32",
             "achieved": achieved_tflops,
-            "peak": PEAK_FP64_TFLOPS,
+            "peak": PEAK_FP32_TFLOPS,
             "unit": "TFLOP/s",
-            "frac": achieved_tflops / PEAK_FP64_TFLOPS,
+            "frac": achieved_tflops / PEAK_FP32_TFLOPS,
             "traffic": traffic,
             "traffic_unit": "bytes per launch (rocprofv3 PMC, %s)" % (pmc[-1] if pmc else "none"),
             "algorithmic": "%d flop per (candidate, node) pair; %d pairs over %d launches" % (
