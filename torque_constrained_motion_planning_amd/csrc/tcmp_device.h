@@ -744,23 +744,16 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
 
 // Returns collision flag; all lanes must call.  `active` lanes only contribute.
 //
-// Phase A (every step): the link frames are generated in a runtime loop over the 10 links and
-// each link's world AABB is tested against each obstacle's world AABB in fp32 (tier 0,
-// branch-free; "maybe" iff the overlap could reach kPen on all three axes -- AABBs contain
-// the shapes, so a penetration >= kPen always gives a "maybe").  Maybe pairs are queued in
-// this wave's LDS queue as (lane, link, obstacle).
+// Phase A (every step): the 10 link frames are generated incrementally and each link's world
+// AABB is kept in fp32 registers; then every obstacle's world AABB (one LDS broadcast) is
+// tested against all ten (tier 0, branch-free; "maybe" iff the overlap could reach kPen on
+// all three axes -- AABBs contain the shapes, so a penetration >= kPen always gives a
+// "maybe").  Maybe pairs are queued in this wave's LDS queue as (lane, link, obstacle).
 // Phase B (flush, when the queue could overflow and at the end): the queued pairs are
 // processed lane-parallel -- each lane rebuilds its pair's link pose in fp64 from the owning
 // lane's cos/sin and runs tiers 1-3 (classify_pair) -- and the undecided ones go through the
 // wave-cooperative exact test (fp32 first pass, fp64 when near kPen or degenerate).
 // Tiers 0-3 are conservative bounds of the exact test, so the answer is the exact test's.
-__device__ __forceinline__ double sel7(const double v[7], int j) {
-  double r = v[0];
-#pragma unroll
-  for (int k = 1; k < 7; ++k) r = (j == k) ? v[k] : r;
-  return r;
-}
-
 // world frame of `link` (0..9) as collides_wave's phase A builds it, for per-lane links
 __device__ __forceinline__ void link_pose(int link, const double cq[7], const double sq[7],
                                           double Ro[9], double po[3]) {
@@ -884,62 +877,67 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
   };
   // ---- phase A ------------------------------------------------------------------------
   if (live) st.pairs_tested += 10u * (unsigned)sc.n_obs;
-  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
-  double Rh[9], ph[3];
-  for (int link = 0; link < 10; ++link) {  // uniform runtime loop: one copy of the body
-    if (link < 7) {
-      const double cr = kJcr[link], sr = kJsr[link], c = sel7(cq, link), s = sel7(sq, link);
+  // world AABBs of the 10 links in fp32 (centre, half extent + rounding margin)
+  float bc[10][3], bh[10][3];
+  {
+    auto put = [&](int link, const double Rr[9], const double pr[3]) {
+      double wc[3], U[9], aabb[3];
+      link_obb(link, Rr, pr, wc, U, aabb);
+#pragma unroll
+      for (int i = 0; i < 3; ++i) {
+        bc[link][i] = (float)wc[i];
+        bh[link][i] = (float)aabb[i] + 1e-5f;
+      }
+    };
+    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < 7; ++j) {
+      const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
       const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
-      const double t[3] = {kJx[link], kJy[link], kJz[link]};
+      const double t[3] = {kJx[j], kJy[j], kJz[j]};
       frame_step(R, p, Rl, t);
-    } else if (link == 7) {
-      const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-      const double tz[3] = {0, 0, kFlangeZ};
-      frame_step(R, p, I, tz);
-      const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
-      const double z0[3] = {0, 0, 0};
-      frame_step(R, p, Rz, z0);
-#pragma unroll
-      for (int k = 0; k < 9; ++k) Rh[k] = R[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) ph[k] = p[k];
-    } else {
-      const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-      const double tf[3] = {0, link == 8 ? kFingerOpen : -kFingerOpen, kFingerZ};
-#pragma unroll
-      for (int k = 0; k < 9; ++k) R[k] = Rh[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) p[k] = ph[k];
-      frame_step(R, p, I, tf);
+      put(j, R, p);
     }
-    double wc[3], U[9], aabb[3];
-    link_obb(link, R, p, wc, U, aabb);
-    const float wx = (float)wc[0], wy = (float)wc[1], wz = (float)wc[2];
-    const float ax = (float)aabb[0] + 1e-5f, ay = (float)aabb[1] + 1e-5f, az = (float)aabb[2] + 1e-5f;
-    for (int o0 = 0; o0 < sc.n_obs; o0 += 4) {
-      // four obstacles per pass: all LDS reads issued before the first compare
-      unsigned mb = 0;
+    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+    const double tz[3] = {0, 0, kFlangeZ};
+    frame_step(R, p, I, tz);
+    const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
+    const double z0[3] = {0, 0, 0};
+    frame_step(R, p, Rz, z0);
+    put(7, R, p);
+    double Rf[9], pf[3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int o = min(o0 + u, sc.n_obs - 1);
-        const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
-        const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
-        const bool m = ((int)(o0 + u < sc.n_obs) & (int)live & (int)(fabsf(wx - oa.x) <= ax + ob4.x) &
-                        (int)(fabsf(wy - oa.y) <= ay + ob4.y) &
-                        (int)(fabsf(wz - oa.z) <= az + ob4.z)) != 0;
-        mb |= (unsigned)m << u;
-      }
-      if (__ballot(mb != 0u) == 0) continue;
+    for (int k = 0; k < 9; ++k) Rf[k] = R[k];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pf[k] = p[k];
+    const double tl[3] = {0, kFingerOpen, kFingerZ};
+    frame_step(Rf, pf, I, tl);
+    put(8, Rf, pf);
+    const double tr[3] = {0, -kFingerOpen, kFingerZ};
+    frame_step(R, p, I, tr);
+    put(9, R, p);
+  }
+  // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
+  for (int o = 0; o < sc.n_obs; ++o) {
+    const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
+    const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
+    unsigned lm = 0;
+#pragma unroll
+    for (int l = 0; l < 10; ++l)
+      lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
+                       (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
+                       (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
+    if (!live) lm = 0;
+    if (__ballot(lm != 0u) == 0) continue;
 #pragma unroll 1
-      for (int u = 0; u < 4; ++u) {
-        const bool m = (mb >> u) & 1u;
-        const uint64_t bm = __ballot(m);
-        if (bm == 0) continue;
-        if (count + 64 > kQcap) flush();
-        if (m) queue[count + (int)__popcll(bm & ((1ull << lane) - 1ull))] =
-            (unsigned)lane | ((unsigned)link << 6) | ((unsigned)(o0 + u) << 10);
-        count += (int)__popcll(bm);
-      }
+    for (int l = 0; l < 10; ++l) {
+      const bool m = (lm >> l) & 1u;
+      const uint64_t bm = __ballot(m);
+      if (bm == 0) continue;
+      if (count + 64 > kQcap) flush();
+      if (m) queue[count + (int)__popcll(bm & ((1ull << lane) - 1ull))] =
+          (unsigned)lane | ((unsigned)l << 6) | ((unsigned)o << 10);
+      count += (int)__popcll(bm);
     }
   }
   if (count) flush();
