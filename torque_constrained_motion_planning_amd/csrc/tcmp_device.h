@@ -516,12 +516,12 @@ __device__ __forceinline__ float wave_maxf(float x) {
 // few 1e-6 m for coordinates of a few metres), and only results within kExactGuard of kPen
 // are re-evaluated in fp64: the collision decision is always the fp64 one.
 constexpr float kExactGuard = 1e-4f;
-#ifdef TCMP_PROF
-// exact32 outcomes: [0] box-face early exit, [1] facets alone below kPen - guard,
-// [2] full evaluation, [3] degenerate (fp64 fallback)
+#ifdef TCMP_PROF_EXACT
+// exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
+// [3] degenerate (fp64 fallback)
 __device__ unsigned long long g_exact_stats[4];
 #endif
-__device__ __noinline__ float exact_pd_wave32(int link, const Pose pose,
+__device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g) {
   const int lane = lane_id();
   const double* R = pose.R;
@@ -563,7 +563,7 @@ __device__ __noinline__ float exact_pd_wave32(int link, const Pose pose,
                      fminf(mx2 - pc2 + h[2], pc2 + h[2] - mn2)));
   }
   if (pd < P - kExactGuard) {
-#ifdef TCMP_PROF
+#ifdef TCMP_PROF_EXACT
     if (lane == 0) atomicAdd(&g_exact_stats[0], 1ull);
 #endif
     return pd;
@@ -577,48 +577,65 @@ __device__ __noinline__ float exact_pd_wave32(int link, const Pose pose,
                       h[2] * fabsf(n.x * A[2] + n.y * A[5] + n.z * A[8]);
     loc = fminf(loc, n.w - pc + rad);
   }
-#ifdef TCMP_PROF
+  // facet axes are exact overlaps: one below kPen - guard already proves "free"
   {
-    const float lf = wave_minf(loc);
-    if (lane == 0 && lf < P - kExactGuard) atomicAdd(&g_exact_stats[1], 1ull);
-  }
+    const float lf = fminf(pd, wave_minf(loc));
+    if (lf < P - kExactGuard) {
+#ifdef TCMP_PROF_EXACT
+      if (lane == 0) atomicAdd(&g_exact_stats[1], 1ull);
 #endif
+      return lf;
+    }
+  }
   bool deg = false;
-  for (int e = e0 + lane; e < e1; e += 64) {
-    const ushort4 ix = g.eidx[e];
-    const float ax0 = g.verts32[3 * ix.x], ay0 = g.verts32[3 * ix.x + 1], az0 = g.verts32[3 * ix.x + 2];
-    const float ex = g.verts32[3 * ix.y] - ax0, ey = g.verts32[3 * ix.y + 1] - ay0,
-                ez = g.verts32[3 * ix.y + 2] - az0;
-    const float4 n1 = g.planes32[ix.z];
-    const float4 n2 = g.planes32[ix.w];
-    const float el2 = ex * ex + ey * ey + ez * ez;
+  for (int base = e0; base < e1; base += 64) {
+    const int e = base + lane;
+    if (e < e1) {
+      const ushort4 ix = g.eidx[e];
+      const float ax0 = g.verts32[3 * ix.x], ay0 = g.verts32[3 * ix.x + 1], az0 = g.verts32[3 * ix.x + 2];
+      const float ex = g.verts32[3 * ix.y] - ax0, ey = g.verts32[3 * ix.y + 1] - ay0,
+                  ez = g.verts32[3 * ix.y + 2] - az0;
+      const float4 n1 = g.planes32[ix.z];
+      const float4 n2 = g.planes32[ix.w];
+      const float el2 = ex * ex + ey * ey + ez * ez;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const float a0 = A[0 + i], a1 = A[3 + i], a2 = A[6 + i];
-      const float s1 = n1.x * a0 + n1.y * a1 + n1.z * a2;
-      const float s2 = n2.x * a0 + n2.y * a1 + n2.z * a2;
-      deg |= ((int)(fabsf(s1) < 1e-5f) | (int)(fabsf(s2) < 1e-5f)) != 0;
-      if (s1 * s2 < 0.f) {
-        float m0 = ey * a2 - ez * a1, m1 = ez * a0 - ex * a2, m2 = ex * a1 - ey * a0;
-        const float len2 = m0 * m0 + m1 * m1 + m2 * m2;
-        if (len2 < 1e-8f * el2) {
-          deg = true;
-        } else {
-          const float ori = m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z);
-          const float il = rsqrtf(len2);
-          deg |= fabsf(ori) * il < 1e-4f;
-          if (ori < 0.f) { m0 = -m0; m1 = -m1; m2 = -m2; }
-          const float hv = m0 * ax0 + m1 * ay0 + m2 * az0;
-          const float pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
-          const float rad = h[0] * fabsf(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
-                            h[1] * fabsf(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
-                            h[2] * fabsf(m0 * A[2] + m1 * A[5] + m2 * A[8]);
-          loc = fminf(loc, (hv - pc + rad) * il);
+      for (int i = 0; i < 3; ++i) {
+        const float a0 = A[0 + i], a1 = A[3 + i], a2 = A[6 + i];
+        const float s1 = n1.x * a0 + n1.y * a1 + n1.z * a2;
+        const float s2 = n2.x * a0 + n2.y * a1 + n2.z * a2;
+        deg |= ((int)(fabsf(s1) < 1e-5f) | (int)(fabsf(s2) < 1e-5f)) != 0;
+        if (s1 * s2 < 0.f) {
+          float m0 = ey * a2 - ez * a1, m1 = ez * a0 - ex * a2, m2 = ex * a1 - ey * a0;
+          const float len2 = m0 * m0 + m1 * m1 + m2 * m2;
+          if (len2 < 1e-8f * el2) {
+            deg = true;
+          } else {
+            const float ori = m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z);
+            const float il = rsqrtf(len2);
+            deg |= fabsf(ori) * il < 1e-4f;
+            if (ori < 0.f) { m0 = -m0; m1 = -m1; m2 = -m2; }
+            const float hv = m0 * ax0 + m1 * ay0 + m2 * az0;
+            const float pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
+            const float rad = h[0] * fabsf(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
+                              h[1] * fabsf(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
+                              h[2] * fabsf(m0 * A[2] + m1 * A[5] + m2 * A[8]);
+            loc = fminf(loc, (hv - pc + rad) * il);
+          }
         }
       }
     }
+    // early "free" once a trustworthy axis is below kPen - guard (no degenerate axis so far)
+    if (base + 64 < e1 && !__ballot(deg)) {
+      const float lf = fminf(pd, wave_minf(loc));
+      if (lf < P - kExactGuard) {
+#ifdef TCMP_PROF_EXACT
+        if (lane == 0) atomicAdd(&g_exact_stats[2], 1ull);
+#endif
+        return lf;
+      }
+    }
   }
-#ifdef TCMP_PROF
+#ifdef TCMP_PROF_EXACT
   if (lane == 0) atomicAdd(&g_exact_stats[__ballot(deg) ? 3 : 2], 1ull);
 #endif
   if (__ballot(deg)) return __builtin_nanf("");
@@ -877,68 +894,82 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
   };
   // ---- phase A ------------------------------------------------------------------------
   if (live) st.pairs_tested += 10u * (unsigned)sc.n_obs;
-  // world AABBs of the 10 links in fp32 (centre, half extent + rounding margin)
-  float bc[10][3], bh[10][3];
-  {
-    auto put = [&](int link, const double Rr[9], const double pr[3]) {
-      double wc[3], U[9], aabb[3];
-      link_obb(link, Rr, pr, wc, U, aabb);
+  // A queue that fills up is flushed after the loop and phase A resumes at (o_res, l_res);
+  // the link AABBs are rebuilt on resume, so nothing of phase A is live across a flush.
+  int o_res = 0, l_res = 0;
+  while (true) {
+    // world AABBs of the 10 links in fp32 (centre, half extent + rounding margin)
+    float bc[10][3], bh[10][3];
+    {
+      auto put = [&](int link, const double Rr[9], const double pr[3]) {
+        double wc[3], U[9], aabb[3];
+        link_obb(link, Rr, pr, wc, U, aabb);
 #pragma unroll
-      for (int i = 0; i < 3; ++i) {
-        bc[link][i] = (float)wc[i];
-        bh[link][i] = (float)aabb[i] + 1e-5f;
+        for (int i = 0; i < 3; ++i) {
+          bc[link][i] = (float)wc[i];
+          bh[link][i] = (float)aabb[i] + 1e-5f;
+        }
+      };
+      double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+#pragma unroll
+      for (int j = 0; j < 7; ++j) {
+        const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
+        const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+        const double t[3] = {kJx[j], kJy[j], kJz[j]};
+        frame_step(R, p, Rl, t);
+        put(j, R, p);
       }
-    };
-    double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+      const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
+      const double tz[3] = {0, 0, kFlangeZ};
+      frame_step(R, p, I, tz);
+      const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
+      const double z0[3] = {0, 0, 0};
+      frame_step(R, p, Rz, z0);
+      put(7, R, p);
+      double Rf[9], pf[3];
 #pragma unroll
-    for (int j = 0; j < 7; ++j) {
-      const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
-      const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
-      const double t[3] = {kJx[j], kJy[j], kJz[j]};
-      frame_step(R, p, Rl, t);
-      put(j, R, p);
+      for (int k = 0; k < 9; ++k) Rf[k] = R[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pf[k] = p[k];
+      const double tl[3] = {0, kFingerOpen, kFingerZ};
+      frame_step(Rf, pf, I, tl);
+      put(8, Rf, pf);
+      const double tr[3] = {0, -kFingerOpen, kFingerZ};
+      frame_step(R, p, I, tr);
+      put(9, R, p);
     }
-    const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
-    const double tz[3] = {0, 0, kFlangeZ};
-    frame_step(R, p, I, tz);
-    const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
-    const double z0[3] = {0, 0, 0};
-    frame_step(R, p, Rz, z0);
-    put(7, R, p);
-    double Rf[9], pf[3];
+    // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
+    bool full = false;
+    for (int o = o_res; o < sc.n_obs && !full; ++o) {
+      const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
+      const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
+      unsigned lm = 0;
 #pragma unroll
-    for (int k = 0; k < 9; ++k) Rf[k] = R[k];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) pf[k] = p[k];
-    const double tl[3] = {0, kFingerOpen, kFingerZ};
-    frame_step(Rf, pf, I, tl);
-    put(8, Rf, pf);
-    const double tr[3] = {0, -kFingerOpen, kFingerZ};
-    frame_step(R, p, I, tr);
-    put(9, R, p);
-  }
-  // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
-  for (int o = 0; o < sc.n_obs; ++o) {
-    const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
-    const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
-    unsigned lm = 0;
-#pragma unroll
-    for (int l = 0; l < 10; ++l)
-      lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
-                       (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
-                       (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
-    if (!live) lm = 0;
-    if (__ballot(lm != 0u) == 0) continue;
+      for (int l = 0; l < 10; ++l)
+        lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
+                         (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
+                         (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
+      if (!live) lm = 0;
+      if (o == o_res) lm &= ~((1u << l_res) - 1u);  // links already queued before a flush
+      if (__ballot(lm != 0u) == 0) continue;
 #pragma unroll 1
-    for (int l = 0; l < 10; ++l) {
-      const bool m = (lm >> l) & 1u;
-      const uint64_t bm = __ballot(m);
-      if (bm == 0) continue;
-      if (count + 64 > kQcap) flush();
-      if (m) queue[count + (int)__popcll(bm & ((1ull << lane) - 1ull))] =
-          (unsigned)lane | ((unsigned)l << 6) | ((unsigned)o << 10);
-      count += (int)__popcll(bm);
+      for (int l = 0; l < 10; ++l) {
+        const bool m = (lm >> l) & 1u;
+        const uint64_t bm = __ballot(m);
+        if (bm == 0) continue;
+        if (count + 64 > kQcap) {
+          o_res = o;
+          l_res = l;
+          full = true;
+          break;
+        }
+        if (m) queue[count + (int)__popcll(bm & ((1ull << lane) - 1ull))] =
+            (unsigned)lane | ((unsigned)l << 6) | ((unsigned)o << 10);
+        count += (int)__popcll(bm);
+      }
     }
+    if (!full) break;
+    flush();
   }
   if (count) flush();
   __builtin_amdgcn_wave_barrier();

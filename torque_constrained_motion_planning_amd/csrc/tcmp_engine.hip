@@ -1319,7 +1319,7 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   for (int i = 0; i < n; ++i) out[i] = s.prof[i];
-#ifdef TCMP_PROF
+#ifdef TCMP_PROF_EXACT
   unsigned long long ex[4];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
   for (int i = 0; i < 4 && 8 + i < n; ++i) out[8 + i] = ex[i];
