@@ -1322,7 +1322,7 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
 #ifdef TCMP_PROF_EXACT
   unsigned long long ex[4];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
-  for (int i = 0; i < 4 && 8 + i < n; ++i) out[8 + i] = ex[i];
+  for (int i = 0; i < 4 && 12 + i < n; ++i) out[12 + i] = ex[i];
 #endif
   return 0;
 }

@@ -17,8 +17,9 @@
 // neighbour scan itself is exact.  Pruning uses the exact fp64 best, as before.
 //
 // Work distribution: eight queues, one per XCD, each over a contiguous eighth of the
-// Morton-sorted candidates; a wave pulls from its own XCD's queue (HW_REG_XCC_ID) so the
-// nodes one XCD touches stay in its L2, and moves on to the next queue when it runs dry.
+// Morton-sorted candidates; a wave pulls batches of four from its own XCD's queue
+// (HW_REG_XCC_ID) so the nodes one XCD touches stay in its L2, and moves on to the next queue
+// when it runs dry.
 #pragma once
 
 constexpr double kNnU32 = 5.9604644775390625e-08;  // 2^-24
@@ -78,29 +79,62 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
   const float E32 = __double2float_ru(E * (1.0 + 1e-9)), ru32 = __double2float_ru(ru);
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
   unsigned long long pairs = 0, tests = 0;
+#ifdef TCMP_PROF
+  // clocks: [0] setup + home chunk, [1] super-chunk bounds, [2] chunk bounds, [3] chunk scans,
+  // [4] final reduction
+  unsigned long long pc[5] = {0, 0, 0, 0, 0};
+  unsigned long long t0 = clock64();
+#define NN_TICK(k) { const unsigned long long t1 = clock64(); pc[k] += t1 - t0; t0 = t1; }
+#else
+#define NN_TICK(k)
+#endif
+  // Candidates are taken kNnBatch at a time: one atomic per batch, the batch's cperm / home /
+  // candidate rows loaded once by lanes 0..3, and the next batch's atomic issued before this
+  // batch's work so its latency overlaps the first chunk loads.
+  constexpr int kNnBatch = 4;
   int qi = (int)xcc_id(), tried = 0;
-  while (true) {
-    int jq = -1;
+  int jb = -1, jn = 0;
+  auto grab_slow = [&]() {
+    jb = -1;
+    jn = 0;
     while (tried < 8) {
       const int lo = (int)((long long)nb * qi / 8), hi = (int)((long long)nb * (qi + 1) / 8);
       int t = 0;
-      if (lane == 0) t = atomicAdd(&st->nn_queue[qi], 1);
+      if (lane == 0) t = atomicAdd(&st->nn_queue[qi], kNnBatch);
       t = __shfl(t, 0);
       if (lo + t < hi) {
-        jq = lo + t;
-        break;
+        jb = lo + t;
+        jn = min(kNnBatch, hi - jb);
+        return;
       }
       qi = (qi + 1) & 7;
       ++tried;
     }
-    if (jq < 0) break;
-    const int lj = cperm[jq];
+  };
+  grab_slow();
+  while (jb >= 0) {
+    const bool bl = lane < jn;
+    const int ljl = bl ? cperm[jb + lane] : 0;
+    const int hml = bl ? home[jb + lane] : 0;
+    double sl[7];
+    if (bl) {
+      load7(cand + 8 * (size_t)ljl, sl);
+    } else {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) sl[k] = 0.0;
+    }
+    const int qlo = (int)((long long)nb * qi / 8), qhi = (int)((long long)nb * (qi + 1) / 8);
+    int tn = 0;
+    if (lane == 0) tn = atomicAdd(&st->nn_queue[qi], kNnBatch);
+  for (int ib = 0; ib < jn; ++ib) {
+    const int lj = __builtin_amdgcn_readlane(ljl, ib);
     double s[7];
-    load7(cand + 8 * (size_t)lj, s);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) s[k] = readlane_d(sl[k], ib);
     float s32[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) s32[k] = (float)s[k];
-    const int hc = min(nch - 1, home[jq] / kNnC);
+    const int hc = min(nch - 1, __builtin_amdgcn_readlane(hml, ib) / kNnC);
     const int hs = hc / kNnS;
     double b1 = INFINITY, b2 = INFINITY;
     int bi = INT_MAX;
@@ -186,11 +220,13 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
       pairs += (unsigned long long)min((long long)kNnC, T - (long long)hc * kNnC);
       thr = refresh();
     }
+    NN_TICK(0);
     for (int g = 0; g < nsup; g += 64) {
       const int sidx = zigzag(hs, g + lane, nsup);
       const float lbs = sidx >= 0 ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32) : INFINITY;
       tests += (unsigned long long)min(64, nsup - g);
       uint64_t smask = __ballot(lbs <= thr);
+      NN_TICK(1);
       while (smask) {
         const int i = __builtin_ctzll(smask);
         smask &= smask - 1;
@@ -201,6 +237,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
         const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32) : INFINITY;
         tests += (unsigned long long)min(kNnS, nch - S * kNnS);
         uint64_t cmask = __ballot(lbc <= thr);
+        NN_TICK(2);
         while (cmask) {
           auto take = [&]() -> int {
             while (cmask) {
@@ -212,6 +249,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
           };
           const int ca = take(), cb = take(), cc = take(), cd = take();
           if (ca >= 0) thr = scan4(ca, cb, cc, cd);
+          NN_TICK(3);
         }
       }
     }
@@ -229,9 +267,24 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
       nn[lj] = wi == INT_MAX ? 0 : wi;
       if (second) second[lj] = sec;
     }
+    NN_TICK(4);
+  }
+    tn = __shfl(tn, 0);
+    if (qlo + tn < qhi) {
+      jb = qlo + tn;
+      jn = min(kNnBatch, qhi - jb);
+    } else {
+      qi = (qi + 1) & 7;
+      ++tried;
+      grab_slow();
+    }
   }
   if (lane == 0) {
     atomicAdd(&st->nn_pairs, pairs);
     atomicAdd(&st->nn_box_tests, tests);
+#ifdef TCMP_PROF
+    for (int k = 0; k < 5; ++k) atomicAdd(&st->prof[8 + k], pc[k]);
+#endif
   }
+#undef NN_TICK
 }
