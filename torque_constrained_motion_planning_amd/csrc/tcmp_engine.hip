@@ -7,9 +7,11 @@
 //
 // Round structure (batched frontier, B candidates per round, one HIP stream):
 //   k_sample        Philox4x32-10 candidate draws (or host-provided draws)
-//   k_nearest       LDS-tiled brute-force argmin over the tree snapshot (fp64 VALU bound)
+//   nearest         per-round radix-tree cell index of the snapshot (tcmp_nn.h) and the
+//                   pruned exact scan k_nearest_wave32 (tcmp_nn32.h); k_nearest below is
+//                   the brute-force scan behind tcmp_nearest and TCMP_NN_BRUTE=1
 //   k_edges         persistent lane-refill edge walker: extend steps, collision, torque
-//   k_insert        lane-ordered insertion (block scan), goal test
+//   k_ins_*         lane-ordered insertion (device-wide scan), goal test (tcmp_insert.h)
 //   k_rewire_scan   neighbours within radius of each new node (snapshot)
 //   k_rewire_apply  sequential rewire per new node (rrt_star.py:187-192)
 // then k_retrace / k_traj (min-jerk + final dynamic torque validation).
@@ -68,6 +70,7 @@ struct DevState {
   int status;
   int overflow;
   int nn_queue[8];       // per-XCD work queues of k_nearest_wave32
+  int nn_cells;          // cells of the current nearest-neighbour index (k_nn_starts)
   unsigned long long prof[16];  // TCMP_PROF builds: k_edges clock breakdown + exact-test stats
 };
 
@@ -223,16 +226,9 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
 }
 
 // ------------------------------------------------------------------------------------------
-// Morton-chunked exact nearest neighbour.
-// Each round the snapshot is sorted by a 63-bit Morton key (9 bits per joint over the joint
-// limits), cut into 256-node chunks with axis-aligned bounds, and every wave scores 128
-// Morton-sorted candidates against the chunks in zig-zag order from the candidates' own
-// position, skipping a chunk when the box lower bound exceeds every lane's current best
-// (plus the rewire radius, so the second-nearest stays exact within the range k_insert's
-// rewire bound needs).  Ties compare (distance, original index): the first index wins as in
-// rrt_star.py:14, whatever the visiting order.
+// Morton keys of snapshot nodes and candidates (63 bits: 9 per joint over the joint limits)
+// for the nearest-neighbour index (tcmp_nn.h).
 // ------------------------------------------------------------------------------------------
-constexpr int kChunk = 256;
 
 __device__ __forceinline__ unsigned long long morton7(const double q[7]) {
   unsigned u[7];
@@ -275,150 +271,6 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
   vals[j] = j;
 }
 
-#if 0  // first chunked scan (128 candidates per wave), superseded by tcmp_nn.h
-// sorted snapshot: stree[p] = (q0..q6, original index); cbox[c] = (lo0..6, -, hi0..6, -)
-__global__ __launch_bounds__(256) void k_build_chunks(DevState* st, const double* cfg,
-                                                      const int* svals, double* stree,
-                                                      double* cbox) {
-  __shared__ double red[2][7][4];
-  const long long T = st->n_nodes;
-  const long long p = (long long)blockIdx.x * kChunk + threadIdx.x;
-  if ((long long)blockIdx.x * kChunk >= T) return;  // block-uniform
-  double q[7];
-  double lo[7], hi[7];
-  if (p < T) {
-    const int n = svals[p];
-    load7(cfg + 8 * (size_t)n, q);
-    store7(stree + 8 * p, q);
-    stree[8 * p + 7] = (double)n;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) { lo[k] = q[k]; hi[k] = q[k]; }
-  } else {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) { lo[k] = INFINITY; hi[k] = -INFINITY; }
-  }
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    lo[k] = wave_min(lo[k]);
-    hi[k] = wave_max(hi[k]);
-  }
-  const int w = threadIdx.x >> 6;
-  if (lane_id() == 0) {
-#pragma unroll
-    for (int k = 0; k < 7; ++k) { red[0][k][w] = lo[k]; red[1][k][w] = hi[k]; }
-  }
-  __syncthreads();
-  if (threadIdx.x < 7) {
-    const int k = threadIdx.x;
-    double a = red[0][k][0], b = red[1][k][0];
-    for (int i = 1; i < 4; ++i) { a = fmin(a, red[0][k][i]); b = fmax(b, red[1][k][i]); }
-    cbox[16 * (size_t)blockIdx.x + k] = a;
-    cbox[16 * (size_t)blockIdx.x + 8 + k] = b;
-  }
-}
-
-template <bool UW>
-__device__ __forceinline__ void nn_update(const double s[7], const double* nd, double w[7],
-                                          double& b1, double& b2, int& bi, double& thr, double ru) {
-  const double d0 = s[0] - nd[0], d1 = s[1] - nd[1], d2 = s[2] - nd[2], d3 = s[3] - nd[3],
-               d4 = s[4] - nd[4], d5 = s[5] - nd[5], d6 = s[6] - nd[6];
-  double dd;
-  if (UW) {
-    dd = d0 * d0;
-    dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
-    dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
-  } else {
-    dd = w[0] * (d0 * d0);
-    dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
-    dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
-  }
-  if (dd <= b1) {
-    const int idx = (int)nd[7];
-    if (dd < b1 || idx < bi) {
-      b2 = b1;
-      b1 = dd;
-      bi = idx;
-      const double t = sqrt(b1) + ru;
-      thr = t * t * (1.0 + 1e-9) + 1e-300;
-    } else {
-      b2 = fmin(b2, dd);
-    }
-  } else {
-    b2 = fmin(b2, dd);
-  }
-}
-
-template <bool UW>
-__global__ __launch_bounds__(256) void k_nearest_chunked(PlanParams P, DevState* st,
-                                                         const double* stree, const double* cbox,
-                                                         const unsigned long long* skeys,
-                                                         const double* cand, const int* cperm,
-                                                         const unsigned long long* ckeys,
-                                                         int nb, int* nn, double* second) {
-  const int lane = lane_id();
-  const int wave = (int)(((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6);
-  const int base = wave * 128;
-  if (base >= nb) return;  // wave-uniform
-  const long long T = st->n_nodes;
-  const int nc = (int)((T + kChunk - 1) / kChunk);
-  const int j0 = base + lane, j1 = base + 64 + lane;
-  const bool a0 = j0 < nb, a1 = j1 < nb;
-  const int l0 = a0 ? cperm[j0] : 0, l1 = a1 ? cperm[j1] : 0;
-  double s0[7], s1[7];
-  load7(cand + 8 * (size_t)l0, s0);
-  load7(cand + 8 * (size_t)l1, s1);
-  double w[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) w[k] = P.w[k];
-  const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
-  double b10 = INFINITY, b20 = INFINITY, thr0 = INFINITY;
-  double b11 = INFINITY, b21 = INFINITY, thr1 = INFINITY;
-  int bi0 = INT_MAX, bi1 = INT_MAX;
-  // home chunk of the wave: position of its first candidate's key in the sorted snapshot
-  const unsigned long long hk = ckeys[base];
-  long long lo = 0, hi = T;
-  while (lo < hi) {
-    const long long mid = (lo + hi) >> 1;
-    if (skeys[mid] < hk) lo = mid + 1; else hi = mid;
-  }
-  const int c0 = (int)min((long long)nc - 1, lo / kChunk);
-  int up = c0, dn = c0 - 1;
-  bool turn_up = true;
-  unsigned long long scanned = 0, boxes = 0;
-  while (up < nc || dn >= 0) {
-    int c;
-    if ((turn_up && up < nc) || dn < 0) c = up++; else c = dn--;
-    turn_up = !turn_up;
-    const double* bx = cbox + 16 * (size_t)c;
-    double lb0 = 0, lb1 = 0;
-#pragma unroll
-    for (int k = 0; k < 7; ++k) {
-      const double g0 = fmax(0.0, fmax(bx[k] - s0[k], s0[k] - bx[8 + k]));
-      const double g1 = fmax(0.0, fmax(bx[k] - s1[k], s1[k] - bx[8 + k]));
-      lb0 = fma(UW ? g0 : w[k] * g0, g0, lb0);
-      lb1 = fma(UW ? g1 : w[k] * g1, g1, lb1);
-    }
-    ++boxes;
-    const bool need = (a0 && lb0 <= thr0) || (a1 && lb1 <= thr1);
-    if (__ballot(need) == 0) continue;
-    const long long n0 = (long long)c * kChunk, n1 = min(T, n0 + kChunk);
-    for (long long pp = n0; pp < n1; ++pp) {
-      const double* nd = stree + 8 * pp;
-      nn_update<UW>(s0, nd, w, b10, b20, bi0, thr0, ru);
-      nn_update<UW>(s1, nd, w, b11, b21, bi1, thr1, ru);
-    }
-    scanned += (unsigned long long)(n1 - n0);
-  }
-  if (a0) { nn[l0] = bi0 == INT_MAX ? 0 : bi0; if (second) second[l0] = b20; }
-  if (a1) { nn[l1] = bi1 == INT_MAX ? 0 : bi1; if (second) second[l1] = b21; }
-  const unsigned long long act = __popcll(__ballot(a0)) + __popcll(__ballot(a1));
-  if (lane == 0) {
-    atomicAdd(&st->nn_pairs, scanned * act);
-    atomicAdd(&st->nn_box_tests, boxes * act);
-  }
-}
-
-#endif
 #include "tcmp_nn.h"
 #include "tcmp_nn32.h"
 #include "tcmp_insert.h"
@@ -576,91 +428,6 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     atomicAdd(&st->prof[6], c_sincos);
     atomicAdd(&st->prof[7], ss.cyc_t123);
 #endif
-  }
-}
-
-// ------------------------------------------------------------------------------------------
-// k_insert: lane-ordered insertion of accepted edges (rrt_star.py:173-180), one block.
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_insert(PlanParams P, DevState* st, Tree tr,
-                                                 const int* nn, const double* cand,
-                                                 const unsigned char* cgoal, const int* nsafe,
-                                                 const int* nsteps, const double* last, int nb,
-                                                 const double* second, int* rwlist) {
-  __shared__ int scan[1024];
-  __shared__ long long gbest[1024];
-  const int tid = threadIdx.x;
-  const long long T = st->n_nodes;
-  const bool goal_open = st->goal_node < 0;
-  const int chunk = (nb + 1023) / 1024;
-  const int j0 = min(nb, tid * chunk), j1 = min(nb, j0 + chunk);
-  if (tid == 0) st->rw_count = 0;
-  int cnt = 0;
-  for (int j = j0; j < j1; ++j) cnt += nsafe[j] > 0;
-  scan[tid] = cnt;
-  __syncthreads();
-  for (int o = 1; o < 1024; o <<= 1) {
-    const int v = tid >= o ? scan[tid - o] : 0;
-    __syncthreads();
-    scan[tid] += v;
-    __syncthreads();
-  }
-  const int total = scan[1023];
-  long long idx = T + scan[tid] - cnt;
-  long long best = LLONG_MAX;
-  const bool fits = T + total <= P.max_nodes;
-  if (fits) {
-    for (int j = j0; j < j1; ++j) {
-      if (nsafe[j] <= 0) continue;
-      const int par = nn[j];
-      double pc[7], lq[7], tq[7];
-      load7(tr.cfg + 8 * (size_t)par, pc);
-      load7(last + 8 * (size_t)j, lq);
-      load7(cand + 8 * (size_t)j, tq);
-      const double d = distance(pc, lq, P.w);
-      double* dst = tr.cfg + 8 * idx;
-      store7(dst, lq);
-      dst[7] = tr.cfg[8 * (size_t)par + 7] + d;
-      tr.parent[idx] = par;
-      store7(tr.tgt + 8 * idx, tq);
-      tr.meta[idx] = make_int2(nsteps[j], nsafe[j]);
-      if (goal_open && cgoal[j] && distance(lq, P.goal, P.w) < P.goal_tol) best = min(best, idx);
-      {
-        // Rewire neighbours n != nearest of the new node satisfy, by the triangle inequality,
-        // d(n, s) <= d(n, new) + d(new, s) < radius + d(new, s); the nearest itself never
-        // rewires (equal cost).  Only lanes whose second-nearest node passes that bound get
-        // the neighbour scan.  Distances in the metric k_nearest used (unweighted if UW).
-        double e2 = 0;
-#pragma unroll
-        for (int k = 0; k < 7; ++k) {
-          const double d = lq[k] - tq[k];
-          e2 = fma(P.uniform_w ? d : P.w[k] * d, d, e2);
-        }
-        const double r = P.uniform_w ? P.radius / sqrt(P.w[0]) : P.radius;
-        const double t = sqrt(e2) + r;
-        if (second[j] < t * t * (1.0 + 1e-9) + 1e-300) rwlist[atomicAdd(&st->rw_count, 1)] = (int)idx;
-      }
-      ++idx;
-    }
-  }
-  gbest[tid] = best;
-  __syncthreads();
-  for (int o = 512; o >= 1; o >>= 1) {
-    if (tid < o) gbest[tid] = min(gbest[tid], gbest[tid + o]);
-    __syncthreads();
-  }
-  if (tid == 0) {
-    st->snap = T;
-    if (!fits) {
-      st->overflow = 1;
-      st->new_count = 0;
-    } else {
-      st->new_count = total;
-      st->n_nodes = T + total;
-      if (goal_open && gbest[0] != LLONG_MAX) st->goal_node = gbest[0];
-    }
-    st->samples += nb;
-    st->round_goal = INT_MAX;
   }
 }
 
@@ -1108,9 +875,9 @@ struct tcmp_handle {
   DBuf<int> nvals_in, svals, cvals_in, cperm;
   DBuf<double> stree, cbox;
   DBuf<float> stree32;
-  bool nn_fp32 = true;
   DBuf<float> cboxf, sboxf;
   DBuf<int> chome, bcount, boff;
+  DBuf<int> cflag, cid, cstart;
   DBuf<unsigned char> sort_tmp;
   bool nn_brute = false;
   int nn_waves_per_cu = 16;
@@ -1226,12 +993,26 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
                                             h->nvals_in.p, h->svals.p, (int)T_bound, 0, 64,
                                             h->stream));
-  hipLaunchKernelGGL(k_nn_build_chunks, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     h->st, h->cfg.p, h->svals.p, h->stree.p, h->stree32.p, h->cboxf.p);
+  // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
+  hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
+                     h->cfg.p, h->svals.p, h->stree.p, h->stree32.p);
   HIPCHK(hipGetLastError());
-  const long long nsup_bound = (((T_bound + kNnC - 1) / kNnC) + kNnS - 1) / kNnS;
-  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(nsup_bound * 64, 256)), dim3(256), 0,
-                     h->stream, h->st, h->cboxf.p, h->sboxf.p);
+  HIPCHK(hipMemsetAsync(h->cflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
+  hipLaunchKernelGGL(k_nn_cells, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
+                     h->skeys.p, h->cflag.p);
+  HIPCHK(hipGetLastError());
+  tb = h->sort_tmp.n;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->cflag.p, h->cid.p, (int)T_bound,
+                                          h->stream));
+  hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
+                     h->cflag.p, h->cid.p, h->cstart.p);
+  HIPCHK(hipGetLastError());
+  // one wave per cell; the cell count is device-side, so cover the worst case (one per node)
+  hipLaunchKernelGGL(k_nn_cell_boxes, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0, h->stream,
+                     h->st, h->stree.p, h->cstart.p, h->cboxf.p);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(((T_bound + kNnS - 1) / kNnS) * 64, 256)),
+                     dim3(256), 0, h->stream, h->st, h->cboxf.p, h->sboxf.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
                      h->ckeys_in.p, h->cvals_in.p);
@@ -1240,7 +1021,7 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                             h->cvals_in.p, h->cperm.p, nb, 0, 64, h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
-                     h->skeys.p, h->ckeys.p, nb, h->chome.p);
+                     h->skeys.p, h->ckeys.p, h->cid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave
   HIPCHK(hipMemsetAsync(&h->st->nn_counter, 0, sizeof(int), h->stream));
@@ -1250,22 +1031,14 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
   h->mark_begin(F_NNSCAN, &e0);
-  if (h->nn_fp32 && P.uniform_w)
+  if (P.uniform_w)
     hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
                        h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
                        h->chome.p, nb, h->nn.p, h->second.p);
-  else if (h->nn_fp32)
+  else
     hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
                        h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
                        h->chome.p, nb, h->nn.p, h->second.p);
-  else if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest_wave<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
-                       per_wave, h->nn.p, h->second.p);
-  else
-    hipLaunchKernelGGL(k_nearest_wave<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p, h->chome.p, nb,
-                       per_wave, h->nn.p, h->second.p);
   HIPCHK(hipGetLastError());
   h->mark_end(F_NNSCAN, e0);
   return 0;
@@ -1378,7 +1151,6 @@ int tcmp_create(int device, tcmp_handle** out) {
   const char* nb_env = getenv("TCMP_NN_BRUTE");
   h->nn_brute = nb_env && nb_env[0] == '1';
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
-  if (const char* e = getenv("TCMP_NN_FP32")) h->nn_fp32 = e[0] != '0';
   *out = h;
   return 0;
 }
@@ -1408,6 +1180,9 @@ int tcmp_destroy(tcmp_handle* h) {
   h->cboxf.release();
   h->sboxf.release();
   h->chome.release();
+  h->cflag.release();
+  h->cid.release();
+  h->cstart.release();
   h->bcount.release();
   h->boff.release();
   h->sort_tmp.release();
@@ -1727,8 +1502,11 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->svals.ensure(N);
   rc = rc ? rc : h->stree.ensure(N * 8);
   rc = rc ? rc : h->stree32.ensure(N * 8);
-  rc = rc ? rc : h->cboxf.ensure(((N + kNnC - 1) / kNnC + 1) * 16);
-  rc = rc ? rc : h->sboxf.ensure(((N + kNnC * kNnS - 1) / (kNnC * kNnS) + 1) * 16);
+  rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
+  rc = rc ? rc : h->sboxf.ensure(((N + kNnS - 1) / kNnS + 1) * 16);
+  rc = rc ? rc : h->cflag.ensure(N);
+  rc = rc ? rc : h->cid.ensure(N);
+  rc = rc ? rc : h->cstart.ensure(N + 1);
   rc = rc ? rc : h->chome.ensure(B);
   rc = rc ? rc : h->ckeys_in.ensure(B);
   rc = rc ? rc : h->ckeys.ensure(B);
@@ -1740,7 +1518,9 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
                                               h->svals.p, (int)N, 0, 64, h->stream));
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, h->ckeys_in.p, h->ckeys.p, h->cvals_in.p,
                                               h->cperm.p, (int)B, 0, 64, h->stream));
-    rc = h->sort_tmp.ensure(std::max(t1, t2));
+    size_t t3 = 0;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, h->cflag.p, h->cid.p, (int)N, h->stream));
+    rc = h->sort_tmp.ensure(std::max(std::max(t1, t2), t3));
   }
   rc = rc ? rc : h->i0.ensure(2);
   if (rc) return rc;

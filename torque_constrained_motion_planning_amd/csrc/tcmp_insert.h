@@ -2,7 +2,7 @@
 // as a device-wide scan: count per 256-lane block, one-block scan of the counts, then every
 // block writes its nodes at (snapshot size + block offset + in-block rank).  Node order is
 // therefore lane order, exactly as the single-pass reference loop appends them.
-// Included by tcmp_engine.hip after the state types and k_insert.
+// Included by tcmp_engine.hip after the state types.
 #pragma once
 
 __global__ __launch_bounds__(256) void k_ins_count(const int* nsafe, int nb, int* bcount) {
@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_ins_write(PlanParams P, DevState* st, T
   tr.meta[idx] = make_int2(nsteps[j], nsafe[j]);
   if (goal_open && cgoal[j] && distance(lq, P.goal, P.w) < P.goal_tol)
     atomicMin(&st->ins_goal, idx);
-  // rewire bound (see k_insert): neighbour scan only if the second-nearest passes it
+  // rewire bound (tcmp_nn32.h): neighbour scan only if the second-nearest bound passes it
   double e2 = 0;
 #pragma unroll
   for (int k = 0; k < 7; ++k) {

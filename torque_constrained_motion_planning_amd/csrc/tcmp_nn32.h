@@ -37,11 +37,14 @@ __device__ __forceinline__ unsigned xcc_id() {
 // the fp64 value box_lb<UW> would give: each gap is shrunk by 1e-6 (> the fp32 rounding of
 // s and of the subtraction for |q| <= kNnCoordMax) and the sum by 1e-6 relative.
 template <bool UW>
-__device__ __forceinline__ float box_lb32(const float* b, const float s[7], const float w[7]) {
+__device__ __forceinline__ float box_lb32(const float* b, const float s[7], const float w[7],
+                                          int* start = nullptr, int* count = nullptr) {
   const float4 l0 = *reinterpret_cast<const float4*>(b);
   const float4 l1 = *reinterpret_cast<const float4*>(b + 4);
   const float4 h0 = *reinterpret_cast<const float4*>(b + 8);
   const float4 h1 = *reinterpret_cast<const float4*>(b + 12);
+  if (start) *start = __float_as_int(l1.w);
+  if (count) *count = __float_as_int(h1.w);
   const float lo[7] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z};
   const float hi[7] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z};
   float lb = 0.f;
@@ -65,7 +68,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
                                                         int* nn, double* second) {
   const int lane = lane_id();
   const long long T = st->n_nodes;
-  const int nch = (int)((T + kNnC - 1) / kNnC), nsup = (nch + kNnS - 1) / kNnS;
+  const int nch = st->nn_cells, nsup = (nch + kNnS - 1) / kNnS;
   double w[7], wsum = 0;
   float w32[7];
 #pragma unroll
@@ -116,6 +119,8 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     const bool bl = lane < jn;
     const int ljl = bl ? cperm[jb + lane] : 0;
     const int hml = bl ? home[jb + lane] : 0;
+    const int hsl = bl ? __float_as_int(cbox[16 * (size_t)hml + 7]) : 0;
+    const int hnl = bl ? __float_as_int(cbox[16 * (size_t)hml + 15]) : 0;
     double sl[7];
     if (bl) {
       load7(cand + 8 * (size_t)ljl, sl);
@@ -134,7 +139,8 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     float s32[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) s32[k] = (float)s[k];
-    const int hc = min(nch - 1, __builtin_amdgcn_readlane(hml, ib) / kNnC);
+    const int hc = __builtin_amdgcn_readlane(hml, ib);
+    const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
     const int hs = hc / kNnS;
     double b1 = INFINITY, b2 = INFINITY;
     int bi = INT_MAX;
@@ -193,31 +199,30 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
       Rf = tr * tr * kRfac;
       return t * t * 1.000003f;
     };
-    auto scan4 = [&](int c0, int c1, int c2, int c3) {
-      const int cs[4] = {c0, c1, c2, c3};
+    // up to four cells (count 0 = none), all row loads in flight before any use
+    auto scan4 = [&](const int cs[4], const int cn[4]) {
       float4 A[4], Bq[4];
       bool val[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const long long n = (long long)cs[u] * kNnC + lane;
-        val[u] = cs[u] >= 0 && n < T;
+        const long long n = (long long)cs[u] + lane;
+        val[u] = lane < cn[u];
         if (val[u]) {
           A[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n);
           Bq[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n + 4);
         }
-        if (cs[u] >= 0) pairs += (unsigned long long)min((long long)kNnC, T - (long long)cs[u] * kNnC);
+        pairs += (unsigned long long)cn[u];
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
-        if (val[u]) upd(A[u], Bq[u], (long long)cs[u] * kNnC + lane);
+        if (val[u]) upd(A[u], Bq[u], (long long)cs[u] + lane);
       return refresh();
     };
     float thr;
     {
-      // home chunk: R = inf, every node exact
-      const long long n = (long long)hc * kNnC + lane;
-      if (n < T) refine(n);
-      pairs += (unsigned long long)min((long long)kNnC, T - (long long)hc * kNnC);
+      // home cell: R = inf, every node exact
+      if (lane < hcn) refine((long long)hcs + lane);
+      pairs += (unsigned long long)hcn;
       thr = refresh();
     }
     NN_TICK(0);
@@ -234,21 +239,28 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
         const int S = __builtin_amdgcn_readlane(sidx, i);
         const int c = S * kNnS + lane;
         const bool cv = c < nch && c != hc;
-        const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32) : INFINITY;
+        int cst = 0, ccn = 0;
+        const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, &cst, &ccn) : INFINITY;
         tests += (unsigned long long)min(kNnS, nch - S * kNnS);
         uint64_t cmask = __ballot(lbc <= thr);
         NN_TICK(2);
         while (cmask) {
-          auto take = [&]() -> int {
+          int cs4[4], cn4[4];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            cs4[u] = 0;
+            cn4[u] = 0;
             while (cmask) {
               const int k = __builtin_ctzll(cmask);
               cmask &= cmask - 1;
-              if (readlane_f(lbc, k) <= thr) return S * kNnS + k;
+              if (readlane_f(lbc, k) <= thr) {
+                cs4[u] = __builtin_amdgcn_readlane(cst, k);
+                cn4[u] = __builtin_amdgcn_readlane(ccn, k);
+                break;
+              }
             }
-            return -1;
-          };
-          const int ca = take(), cb = take(), cc = take(), cd = take();
-          if (ca >= 0) thr = scan4(ca, cb, cc, cd);
+          }
+          if (cn4[0] > 0) thr = scan4(cs4, cn4);
           NN_TICK(3);
         }
       }
