@@ -71,6 +71,7 @@ struct DevState {
   int overflow;
   int nn_queue[8];       // per-XCD work queues of k_nearest_wave32
   int nn_cells;          // cells of the current nearest-neighbour index (k_nn_starts)
+  int nn_supers;         // super-cells of the index
   unsigned long long prof[16];  // TCMP_PROF builds: k_edges clock breakdown + exact-test stats
 };
 
@@ -877,7 +878,8 @@ struct tcmp_handle {
   DBuf<float> stree32;
   DBuf<float> cboxf, sboxf;
   DBuf<int> chome, bcount, boff;
-  DBuf<int> cflag, cid, cstart;
+  DBuf<int> cflag, cid, cstart, sflag, sid, sstart;
+  DBuf<unsigned long long> ckey;
   DBuf<unsigned char> sort_tmp;
   bool nn_brute = false;
   int nn_waves_per_cu = 16;
@@ -998,21 +1000,34 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
                      h->cfg.p, h->svals.p, h->stree.p, h->stree32.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(h->cflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
-  hipLaunchKernelGGL(k_nn_cells, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
-                     h->skeys.p, h->cflag.p);
+  hipLaunchKernelGGL(k_nn_cut<kNnC>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
+                     &h->st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
   HIPCHK(hipGetLastError());
   tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->cflag.p, h->cid.p, (int)T_bound,
                                           h->stream));
-  hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
-                     h->cflag.p, h->cid.p, h->cstart.p);
+  hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
+                     &h->st->n_nodes, (const int*)nullptr, h->cflag.p, h->cid.p, h->cstart.p,
+                     &h->st->nn_cells);
   HIPCHK(hipGetLastError());
   // one wave per cell; the cell count is device-side, so cover the worst case (one per node)
   hipLaunchKernelGGL(k_nn_cell_boxes, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0, h->stream,
-                     h->st, h->stree.p, h->cstart.p, h->cboxf.p);
+                     h->st, h->stree.p, h->cstart.p, h->skeys.p, h->cboxf.p, h->ckey.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(((T_bound + kNnS - 1) / kNnS) * 64, 256)),
-                     dim3(256), 0, h->stream, h->st, h->cboxf.p, h->sboxf.p);
+  // super-cells: the same radix-tree cut over the cells' first keys
+  HIPCHK(hipMemsetAsync(h->sflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
+  hipLaunchKernelGGL(k_nn_cut<kNnS>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
+                     (const long long*)nullptr, &h->st->nn_cells, h->ckey.p, h->sflag.p);
+  HIPCHK(hipGetLastError());
+  tb = h->sort_tmp.n;
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->sflag.p, h->sid.p, (int)T_bound,
+                                          h->stream));
+  hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
+                     (const long long*)nullptr, &h->st->nn_cells, h->sflag.p, h->sid.p,
+                     h->sstart.p, &h->st->nn_supers);
+  HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0,
+                     h->stream, h->st, h->sstart.p, h->cboxf.p, h->sboxf.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
                      h->ckeys_in.p, h->cvals_in.p);
@@ -1021,7 +1036,7 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                             h->cvals_in.p, h->cperm.p, nb, 0, 64, h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
-                     h->skeys.p, h->ckeys.p, h->cid.p, nb, h->chome.p);
+                     h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave
   HIPCHK(hipMemsetAsync(&h->st->nn_counter, 0, sizeof(int), h->stream));
@@ -1183,6 +1198,10 @@ int tcmp_destroy(tcmp_handle* h) {
   h->cflag.release();
   h->cid.release();
   h->cstart.release();
+  h->sflag.release();
+  h->sid.release();
+  h->sstart.release();
+  h->ckey.release();
   h->bcount.release();
   h->boff.release();
   h->sort_tmp.release();
@@ -1503,11 +1522,15 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->stree.ensure(N * 8);
   rc = rc ? rc : h->stree32.ensure(N * 8);
   rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
-  rc = rc ? rc : h->sboxf.ensure(((N + kNnS - 1) / kNnS + 1) * 16);
+  rc = rc ? rc : h->sboxf.ensure((N + 1) * 16);
   rc = rc ? rc : h->cflag.ensure(N);
   rc = rc ? rc : h->cid.ensure(N);
   rc = rc ? rc : h->cstart.ensure(N + 1);
-  rc = rc ? rc : h->chome.ensure(B);
+  rc = rc ? rc : h->sflag.ensure(N);
+  rc = rc ? rc : h->sid.ensure(N);
+  rc = rc ? rc : h->sstart.ensure(N + 1);
+  rc = rc ? rc : h->ckey.ensure(N);
+  rc = rc ? rc : h->chome.ensure(2 * B);
   rc = rc ? rc : h->ckeys_in.ensure(B);
   rc = rc ? rc : h->ckeys.ensure(B);
   rc = rc ? rc : h->cvals_in.ensure(B);

@@ -5,7 +5,7 @@
 // Build, once per round:
 //   1. k_node_keys + radix sort: 63-bit Morton keys (9 bits per joint) of the snapshot nodes.
 //   2. k_nn_rows: stree [T][8] f64 (q0..q6, original index) and stree32 [T][8] f32 in key order.
-//   3. k_nn_cells: the implicit binary radix tree of the sorted keys (Karras 2012: every
+//   3. k_nn_cut<kNnC>: the implicit binary radix tree of the sorted keys (Karras 2012: every
 //      internal node's key range from its neighbours' common-prefix lengths) cut into
 //      "cells": the largest radix-tree subtrees holding at most kNnC nodes.  A cell is a
 //      contiguous key range that is also an axis-aligned Morton cell, so its bounding box is
@@ -13,7 +13,8 @@
 //      half the joint range.  Each cell start is flagged; an inclusive scan numbers the cells.
 //   4. k_nn_starts / k_nn_cell_boxes: per cell its start, node count and f32 bounding box
 //      (lo rounded down, hi rounded up): cbox [C][16] = lo0..6, start, hi0..6, count.
-//   5. k_nn_build_supers: super-cells = 64 consecutive cells, their f32 bounds.
+//   5. k_nn_cut<kNnS> over the cells' first keys: super-cells = radix-tree subtrees of <= 64
+//      cells (compact too); k_nn_build_supers: their f32 bounds, first cell and cell count.
 //   6. candidates: Morton keys, sorted; k_nn_home finds each candidate's home cell.
 #pragma once
 
@@ -46,10 +47,13 @@ __device__ __forceinline__ int nn_delta(const unsigned long long* k, long long T
 }
 
 // internal node i of the radix tree over keys[0, T): its range and split (Karras 2012, §4);
-// flags the start of every child range of <= kNnC keys whose parent holds more
-__global__ __launch_bounds__(256) void k_nn_cells(DevState* st, const unsigned long long* keys,
-                                                  int* flag) {
-  const long long T = st->n_nodes;
+// flags the start of every child range of <= cap keys whose parent holds more.  Used twice:
+// over the node keys (cells of <= kNnC nodes) and over the cells' first keys (super-cells of
+// <= kNnS cells).  *count is the device-side number of keys.
+template <int cap>
+__global__ __launch_bounds__(256) void k_nn_cut(const long long* count_ll, const int* count_i,
+                                                const unsigned long long* keys, int* flag) {
+  const long long T = count_ll ? *count_ll : (long long)*count_i;
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i == 0) flag[0] = 1;
   if (i >= T - 1) return;
@@ -69,27 +73,31 @@ __global__ __launch_bounds__(256) void k_nn_cells(DevState* st, const unsigned l
   }
   const long long g = i + s * d + min(d, 0);
   const long long a = min(i, j), b = max(i, j);
-  if (b - a + 1 <= kNnC) return;           // not a parent of a cell
-  if (g - a + 1 <= kNnC) flag[a] = 1;      // left child is a cell
-  if (b - g <= kNnC) flag[g + 1] = 1;      // right child is a cell
+  if (b - a + 1 <= cap) return;           // not a parent of a cut subtree
+  if (g - a + 1 <= cap) flag[a] = 1;      // left child is cut
+  if (b - g <= cap) flag[g + 1] = 1;      // right child is cut
 }
 
-// cid = inclusive scan of flag: cell of position p is cid[p] - 1
-__global__ __launch_bounds__(256) void k_nn_starts(DevState* st, const int* flag, const int* cid,
-                                                   int* cstart) {
-  const long long T = st->n_nodes;
+// cid = inclusive scan of flag: group of position p is cid[p] - 1; writes the group starts
+// and the group count
+__global__ __launch_bounds__(256) void k_nn_starts(const long long* count_ll, const int* count_i,
+                                                   const int* flag, const int* cid, int* cstart,
+                                                   int* groups) {
+  const long long T = count_ll ? *count_ll : (long long)*count_i;
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
   if (p >= T) return;
   if (flag[p]) cstart[cid[p] - 1] = (int)p;
   if (p == T - 1) {
     cstart[cid[p]] = (int)T;
-    st->nn_cells = cid[p];
+    *groups = cid[p];
   }
 }
 
-// one wave per cell: bounds of its rows
+// one wave per cell: bounds of its rows; also the cell's first key (for the super-cell cut)
 __global__ __launch_bounds__(256) void k_nn_cell_boxes(DevState* st, const double* stree,
-                                                       const int* cstart, float* cbox) {
+                                                       const int* cstart,
+                                                       const unsigned long long* skeys,
+                                                       float* cbox, unsigned long long* ckey) {
   const int C = st->nn_cells;
   const long long c = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
   if (c >= C) return;  // wave-uniform
@@ -119,20 +127,24 @@ __global__ __launch_bounds__(256) void k_nn_cell_boxes(DevState* st, const doubl
     }
     bx[7] = __int_as_float(a);
     bx[15] = __int_as_float(b - a);
+    ckey[c] = skeys[a];
   }
 }
 
-__global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const float* cbox,
-                                                         float* sbox) {
-  const long long nch = st->nn_cells, nsup = (nch + kNnS - 1) / kNnS;
+// one wave per super-cell (a radix-tree subtree of <= kNnS cells): union of its cells' bounds;
+// sbox [S][16] = lo0..6, first cell, hi0..6, cell count
+__global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const int* sstart,
+                                                         const float* cbox, float* sbox) {
+  const int nsup = st->nn_supers;
   const long long sw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   if (sw >= nsup) return;  // wave-uniform
-  const long long c = sw * kNnS + lane_id();
+  const int c0 = sstart[sw], c1 = sstart[sw + 1];
+  const long long c = c0 + lane_id();
   float lo[7], hi[7];
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
-    lo[k] = c < nch ? cbox[16 * c + k] : INFINITY;
-    hi[k] = c < nch ? cbox[16 * c + 8 + k] : -INFINITY;
+    lo[k] = c < c1 ? cbox[16 * c + k] : INFINITY;
+    hi[k] = c < c1 ? cbox[16 * c + 8 + k] : -INFINITY;
   }
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
@@ -145,14 +157,16 @@ __global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const flo
       sbox[16 * sw + k] = lo[k];
       sbox[16 * sw + 8 + k] = hi[k];
     }
-    sbox[16 * sw + 7] = 0.f;
-    sbox[16 * sw + 15] = 0.f;
+    sbox[16 * sw + 7] = __int_as_float(c0);
+    sbox[16 * sw + 15] = __int_as_float(c1 - c0);
   }
 }
 
-// home cell of each Morton-sorted candidate: the cell holding its key's lower bound
+// home cell of each Morton-sorted candidate: the cell holding its key's lower bound, and its
+// super-cell: home[j] = cell, home[nb + j] = super-cell
 __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
-                          const unsigned long long* ckeys, const int* cid, int nb, int* home) {
+                          const unsigned long long* ckeys, const int* cid, const int* sid, int nb,
+                          int* home) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
   const long long T = st->n_nodes;
@@ -162,7 +176,9 @@ __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
     const long long mid = (lo + hi) >> 1;
     if (skeys[mid] < k) lo = mid + 1; else hi = mid;
   }
-  home[j] = cid[min(lo, T - 1)] - 1;
+  const int c = cid[min(lo, T - 1)] - 1;
+  home[j] = c;
+  home[nb + j] = sid[c] - 1;
 }
 
 // position p of the zig-zag walk out from h over [0, n): h, h+1, h-1, h+2, h-2, ...;

@@ -68,7 +68,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
                                                         int* nn, double* second) {
   const int lane = lane_id();
   const long long T = st->n_nodes;
-  const int nch = st->nn_cells, nsup = (nch + kNnS - 1) / kNnS;
+  const int nch = st->nn_cells, nsup = st->nn_supers;
   double w[7], wsum = 0;
   float w32[7];
 #pragma unroll
@@ -119,6 +119,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     const bool bl = lane < jn;
     const int ljl = bl ? cperm[jb + lane] : 0;
     const int hml = bl ? home[jb + lane] : 0;
+    const int hsu = bl ? home[nb + jb + lane] : 0;
     const int hsl = bl ? __float_as_int(cbox[16 * (size_t)hml + 7]) : 0;
     const int hnl = bl ? __float_as_int(cbox[16 * (size_t)hml + 15]) : 0;
     double sl[7];
@@ -141,7 +142,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     for (int k = 0; k < 7; ++k) s32[k] = (float)s[k];
     const int hc = __builtin_amdgcn_readlane(hml, ib);
     const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
-    const int hs = hc / kNnS;
+    const int hs = __builtin_amdgcn_readlane(hsu, ib);
     double b1 = INFINITY, b2 = INFINITY;
     int bi = INT_MAX;
     float r2 = INFINITY;   // smallest fp32 value among this lane's unrefined nodes
@@ -228,7 +229,9 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     NN_TICK(0);
     for (int g = 0; g < nsup; g += 64) {
       const int sidx = zigzag(hs, g + lane, nsup);
-      const float lbs = sidx >= 0 ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32) : INFINITY;
+      int sc0 = 0, scn = 0;
+      const float lbs =
+          sidx >= 0 ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, &sc0, &scn) : INFINITY;
       tests += (unsigned long long)min(64, nsup - g);
       uint64_t smask = __ballot(lbs <= thr);
       NN_TICK(1);
@@ -236,12 +239,12 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
         const int i = __builtin_ctzll(smask);
         smask &= smask - 1;
         if (readlane_f(lbs, i) > thr) continue;
-        const int S = __builtin_amdgcn_readlane(sidx, i);
-        const int c = S * kNnS + lane;
-        const bool cv = c < nch && c != hc;
+        const int S0 = __builtin_amdgcn_readlane(sc0, i), Sn = __builtin_amdgcn_readlane(scn, i);
+        const int c = S0 + lane;
+        const bool cv = lane < Sn && c != hc;
         int cst = 0, ccn = 0;
         const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, &cst, &ccn) : INFINITY;
-        tests += (unsigned long long)min(kNnS, nch - S * kNnS);
+        tests += (unsigned long long)Sn;
         uint64_t cmask = __ballot(lbc <= thr);
         NN_TICK(2);
         while (cmask) {
