@@ -227,9 +227,12 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
 }
 
 // ------------------------------------------------------------------------------------------
-// Morton keys of snapshot nodes and candidates (63 bits: 9 per joint over the joint limits)
-// for the nearest-neighbour index (tcmp_nn.h).
+// Morton keys of snapshot nodes and candidates for the nearest-neighbour index (tcmp_nn.h):
+// 9 bits per joint over the joint limits, interleaved, and only the top kKeyBits kept --
+// 2^36 cells leave at most a handful of nodes per cell, and the radix sorts run 5 digit
+// passes instead of 8.
 // ------------------------------------------------------------------------------------------
+constexpr int kKeyBits = 36;
 
 __device__ __forceinline__ unsigned long long morton7(const double q[7]) {
   unsigned u[7];
@@ -252,11 +255,11 @@ __global__ void k_node_keys(DevState* st, const double* cfg, long long T_bound,
   const long long T = st->n_nodes;
   for (long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x; n < T_bound;
        n += (long long)gridDim.x * blockDim.x) {
-    unsigned long long key = ~0ull;
+    unsigned long long key = (1ull << kKeyBits);  // past every real key: sorts last
     if (n < T) {
       double q[7];
       load7(cfg + 8 * n, q);
-      key = morton7(q);
+      key = morton7(q) >> (63 - kKeyBits);
     }
     keys[n] = key;
     vals[n] = (int)n;
@@ -268,7 +271,7 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
   if (j >= nb) return;
   double q[7];
   load7(cand + 8 * (size_t)j, q);
-  keys[j] = morton7(q);
+  keys[j] = morton7(q) >> (63 - kKeyBits);
   vals[j] = j;
 }
 
@@ -993,8 +996,8 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipGetLastError());
   size_t tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
-                                            h->nvals_in.p, h->svals.p, (int)T_bound, 0, 64,
-                                            h->stream));
+                                            h->nvals_in.p, h->svals.p, (int)T_bound, 0,
+                                            kKeyBits + 1, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
                      h->cfg.p, h->svals.p, h->stree.p, h->stree32.p);
@@ -1034,7 +1037,8 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(hipGetLastError());
   tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
-                                            h->cvals_in.p, h->cperm.p, nb, 0, 64, h->stream));
+                                            h->cvals_in.p, h->cperm.p, nb, 0, kKeyBits + 1,
+                                            h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
                      h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
