@@ -31,8 +31,27 @@ from torque_constrained_motion_planning_amd.scene import obstacle_array, random_
 START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])  # utils.py:45
 PEAK_FP32_TFLOPS = 157.3    # MI355X fp32 vector peak (spec, MI355X_MICROARCH.md)
 PEAK_HBM_GBS = 8000.0       # MI355X HBM3E peak (MI355X_MICROARCH.md)
+PEAK_FP64_TFLOPS = 78.6     # MI355X fp64 vector peak (spec)
 NN_FLOP_PER_PAIR = 21       # 7 sub + 7 fma per (candidate, node) pair, fp32 first pass (SURVEY 8d F_nn)
-NN_BYTES_PER_NODE = 64      # one tree record (q0..q6, cost) streamed per block
+# SURVEY 8d per-edge-step work: FK, link-vs-box cull per (link, obstacle), static RNE (rne and
+# nov during search), SAT per pair surviving the cull
+F_FK, F_BP, F_RNE_STATIC, F_SAT, N_LINKS = 720, 48, 3000, 260, 10
+
+
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
+    workload (profiles/*_pmc_hbm.json): 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE."""
+    prof = os.path.join(REPO, "profiles")
+    pmc = sorted(f for f in os.listdir(prof) if f.endswith("_pmc_hbm.json")) \
+        if os.path.isdir(prof) else []
+    if not pmc:
+        return None
+    d = json.load(open(os.path.join(prof, pmc[-1])))["dispatches"].get(kernel, [])
+    fetch = [x["value_KiB"] for x in d if x["counter"] == "FETCH_SIZE"]
+    write = [x["value_KiB"] for x in d if x["counter"] == "WRITE_SIZE"]
+    if not fetch or len(fetch) != len(write):
+        return None
+    return (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
 
 
 def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None):
@@ -78,18 +97,39 @@ def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass
     return r, out
 
 
-def cpu_baseline(obs, goal, n_samples, seed, mode=2, mass=5.0):
+def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0):
     """Oracle (C restatement of the reference loop, B = 1 = rrt_star.py semantics) on the
-    same scene and Philox sample stream, single core."""
+    same scene and Philox sample stream: single core in-process, then one independent query
+    per host core (separate worker processes that never touch the GPU).  The all-core rate
+    is the reported value (SURVEY 8d / BASELINE.md CPU-baseline plan)."""
+    import subprocess
+    import tempfile
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     t0 = time.perf_counter()
     ref = O.rrt_run(START, goal, n_samples, obs, mode, mass, 5.0, batch=1, seed=seed, cull=2)
-    dt = time.perf_counter() - t0
-    return {"value": n_samples / dt, "unit": "samples/s", "cores": 1, "kind": "port",
-            "sample": "oracle/tcmp_oracle.c sequential RRT* (B=1, reference loop semantics), "
-                      "first %d samples of the same C3 query (16 boxes, 5 kg, rne), %.1f s, "
-                      "%d nodes, %d extend steps" % (n_samples, dt, ref["n_nodes"], ref["edge_steps"])}
+    dt1 = time.perf_counter() - t0
+    single = n_samples / dt1
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "scene.npz")
+        np.savez(path, start=START, goal=goal, obs=obs, mode=mode, mass=mass)
+        worker = os.path.join(REPO, "oracle", "bench_worker.py")
+        t0 = time.perf_counter()
+        procs = [subprocess.Popen([sys.executable, worker, path, str(n_samples), str(seed + 1 + i)],
+                                  stdout=subprocess.PIPE, stderr=subprocess.DEVNULL)
+                 for i in range(workers)]
+        outs = [p.communicate()[0] for p in procs]
+        dtw = time.perf_counter() - t0
+        done = [json.loads(o) for o, p in zip(outs, procs) if p.returncode == 0 and o.strip()]
+    multi = sum(d["samples"] for d in done) / dtw if done else None
+    return {"value": multi if multi else single, "unit": "samples/s",
+            "cores": len(done) if multi else 1, "kind": "port",
+            "single_core": single,
+            "sample": "oracle/tcmp_oracle.c sequential RRT* (B=1, reference loop semantics) on the "
+                      "same C3 scene (16 boxes, 5 kg, rne): %d samples per query; single core "
+                      "%.1f s (%d nodes, %d extend steps); %d independent queries, one per core, "
+                      "%.1f s wall" % (n_samples, dt1, ref["n_nodes"], ref["edge_steps"],
+                                       len(done), dtw)}
 
 
 def main():
@@ -100,7 +140,9 @@ def main():
     ap.add_argument("--samples", type=int, default=1_000_000)
     ap.add_argument("--batch", type=int, default=262144)
     ap.add_argument("--obstacles", type=int, default=16)
-    ap.add_argument("--cpu-samples", type=int, default=50000)
+    ap.add_argument("--cpu-samples", type=int, default=40000)
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
+                    help="host cores for the multi-core CPU baseline (16 = one GPU's share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args()
@@ -154,29 +196,49 @@ def main():
         dt = float(t.item())
 
     total_samples = args.samples * args.steps * world
-    # dominant kernel: k_nearest_wave32 (pruned Morton-chunk argmin over the snapshot, fp32
-    # first pass + exact fp64 refinement); ms_nn_scan = hipEvents around its launches only,
-    # on the engine's stream.  Achieved = 21 flop x evaluated pairs / scan time.
-    nn_pairs = sum(x["nn_pairs"] for x in results)
-    nn_ms = sum(x["ms_nn_scan"] for x in results)
-    nn_launches = sum(x["launches_nearest"] for x in results)
-    achieved_tflops = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
-    # HBM traffic per k_nearest_wave32 launch from the committed rocprofv3 PMC passes of this same
-    # workload (profiles/*_pmc_hbm.json; FETCH_SIZE doubled per the gfx950 correction)
-    traffic = None
-    pmc = sorted(f for f in os.listdir(os.path.join(REPO, "profiles")) if f.endswith("_pmc_hbm.json")) \
-        if os.path.isdir(os.path.join(REPO, "profiles")) else []
-    if pmc:
-        d = json.load(open(os.path.join(REPO, "profiles", pmc[-1])))["dispatches"].get(
-            "k_nearest_wave32", [])
-        fetch = [x["value_KiB"] for x in d if x["counter"] == "FETCH_SIZE"]
-        write = [x["value_KiB"] for x in d if x["counter"] == "WRITE_SIZE"]
-        if fetch and len(fetch) == len(write):
-            traffic = (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
-    kernel_ms = {k: sum(x[k] for x in results) / args.steps for k in
+    S = args.steps
+    kernel_ms = {k: sum(x[k] for x in results) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
     if args.verbose and rank == 0:
         print(json.dumps({"per_step": results, "kernel_ms_per_step": kernel_ms}), file=sys.stderr)
+    launches = sum(x["launches_nearest"] for x in results)  # one k_edges and one nearest scan per round
+
+    # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
+    # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
+    # search never touches, so it is reported beside it, not as "achieved".
+    nn_pairs = sum(x["nn_pairs"] for x in results)
+    nn_full = sum(x["nn_full_pairs"] for x in results)
+    nn_ms = sum(x["ms_nn_scan"] for x in results)
+    nn_tf = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
+    roof_nn = {
+        "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, launches),
+        "bound": "valu_fp32", "achieved": nn_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+        "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32"),
+        "algorithmic": "%d flop per evaluated (candidate, node) pair; %d pairs over %d launches "
+                       "(brute force would be %d pairs: %.1f PFLOP/s equivalent)" % (
+                           NN_FLOP_PER_PAIR, nn_pairs, launches, nn_full,
+                           NN_FLOP_PER_PAIR * nn_full / (nn_ms * 1e-3) / 1e15 if nn_ms else 0.0)}
+    # k_edges: SURVEY 8d per-step work F_fk + F_bp * L * n_obs + F_rne, + F_sat per pair that
+    # survives the cull (device counters), fp64 VALU
+    steps = sum(x["edge_steps"] for x in results)
+    sat = sum(x["pairs_sat"] for x in results)
+    edge_flop = steps * (F_FK + F_BP * N_LINKS * args.obstacles + F_RNE_STATIC) + F_SAT * sat
+    ed_ms = sum(x["ms_edges"] for x in results)
+    ed_tf = edge_flop / (ed_ms * 1e-3) / 1e12 if ed_ms > 0 else 0.0
+    roof_ed = {
+        "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
+        "bound": "valu_fp64", "achieved": ed_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
+        "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges"),
+        "algorithmic": "per extend step F_fk %d + F_bp %d x %d links x %d obstacles + F_rne %d, "
+                       "+ F_sat %d per pair past the cull; %d steps, %d such pairs, %d launches" % (
+                           F_FK, F_BP, N_LINKS, args.obstacles, F_RNE_STATIC, F_SAT, steps, sat,
+                           launches)}
+    dominant, other = (roof_nn, roof_ed) if nn_ms >= ed_ms else (roof_ed, roof_nn)
+    # north-star HBM figure: compulsory bytes per query = 68 T_r per round (tree read
+    # once) + 72 B_r per round (candidates written) + trajectory rows, over the step time
+    snap = sum(x["snap_sum"] for x in results)
+    hbm_bytes = 68 * snap + 72 * total_samples / world + 22 * 8 * sum(x["n_traj"] for x in results)
+    hbm_gbs = hbm_bytes / (dt / 1.0) / 1e9 * world if dt > 0 else 0.0
 
     line = {
         "metric": "torque-feasible collision-checked RRT* samples/sec, Panda 7-DOF, 1/2/4/8 GPU",
@@ -196,26 +258,20 @@ def main():
                                "GPU per step" % (args.obstacles, args.samples),
                    "batch_per_round": args.batch, "execution_time_s": 5.0,
                    "parallelism": "query-sharded x%d" % world},
-        "roofline": {
-            "kernel": "k_nearest_wave32",
-            "avg_launch_ms": nn_ms / max(1, nn_launches),
-            "bound": "valu_fp32",
-            "achieved": achieved_tflops,
-            "peak": PEAK_FP32_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved_tflops / PEAK_FP32_TFLOPS,
-            "traffic": traffic,
-            "traffic_unit": "bytes per launch (rocprofv3 PMC, %s)" % (pmc[-1] if pmc else "none"),
-            "algorithmic": "%d flop per (candidate, node) pair; %d pairs over %d launches" % (
-                NN_FLOP_PER_PAIR, nn_pairs, nn_launches),
-        },
+        "roofline": dominant,
+        "roofline_other": other,
+        "hbm_roofline": {"bytes_per_step": hbm_bytes / S, "achieved": hbm_gbs, "unit": "GB/s",
+                         "peak": PEAK_HBM_GBS, "frac": hbm_gbs / PEAK_HBM_GBS,
+                         "definition": "SURVEY 8d compulsory bytes: 68 T_r + 72 B_r per round "
+                                       "+ 176 B per trajectory row, whole job"},
         "kernel_ms_per_step": kernel_ms,
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(obs, goal, args.cpu_samples, step_seed(0))
+        line["cpu_baseline"] = cpu_baseline(obs, goal, args.cpu_samples, step_seed(0),
+                                            args.cpu_workers)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

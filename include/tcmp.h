@@ -135,7 +135,9 @@ typedef struct {
   double ms_finish;
   int64_t launches_nearest;
   uint64_t nn_box_tests;  /* (candidate, chunk-box) lower-bound tests of the pruned scan */
-  double ms_nn_scan;      /* the k_nearest_wave launches alone (part of ms_nearest) */
+  double ms_nn_scan;      /* the k_nearest_wave32 launches alone (part of ms_nearest) */
+  uint64_t snap_sum;      /* sum over rounds of the snapshot size T_r */
+  uint64_t nn_full_pairs; /* sum over rounds of T_r * B_r: the brute-force scan's pair count */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

@@ -61,6 +61,8 @@ struct DevState {
   long long W, ni, K, first_fail;
   unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
   unsigned long long nn_box_tests;
+  unsigned long long snap_sum;       // sum over rounds of the snapshot size T_r
+  unsigned long long nn_full_pairs;  // sum over rounds of T_r * B_r (brute-force-equivalent)
   long long ins_total;   // accepted edges of the current round (k_ins_scan)
   long long ins_goal;    // lowest goal-reaching new node of the round (k_ins_write)
   int work_counter;
@@ -1752,6 +1754,8 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   r->launches_nearest = h->launches_nearest;
   r->nn_box_tests = s.nn_box_tests;
   r->ms_nn_scan = h->ms[F_NNSCAN];
+  r->snap_sum = s.snap_sum;
+  r->nn_full_pairs = s.nn_full_pairs;
   return 0;
 }
 

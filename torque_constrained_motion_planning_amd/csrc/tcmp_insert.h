@@ -102,5 +102,7 @@ __global__ void k_ins_final(PlanParams P, DevState* st, int nb) {
     if (st->goal_node < 0 && st->ins_goal != LLONG_MAX) st->goal_node = st->ins_goal;
   }
   st->samples += nb;
+  st->snap_sum += (unsigned long long)T;
+  st->nn_full_pairs += (unsigned long long)T * (unsigned long long)nb;
   st->round_goal = INT_MAX;
 }
