@@ -17,6 +17,7 @@
 // then k_retrace / k_traj (min-jerk + final dynamic torque validation).
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <climits>
@@ -235,6 +236,10 @@ __global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, con
 // passes instead of 8.
 // ------------------------------------------------------------------------------------------
 constexpr int kKeyBits = 36;
+// rocprim picks a block-sort + merge-sort chain (~15 launches) below 1M items by default;
+// the Onesweep radix sort (one histogram pass + one launch per 8-bit digit) is faster here
+using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                           rocprim::default_config, 16384>;
 
 __device__ __forceinline__ unsigned long long morton7(const double q[7]) {
   unsigned u[7];
@@ -997,9 +1002,9 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
                      0, h->stream, h->st, h->cfg.p, T_bound, h->nkeys_in.p, h->nvals_in.p);
   HIPCHK(hipGetLastError());
   size_t tb = h->sort_tmp.n;
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
-                                            h->nvals_in.p, h->svals.p, (int)T_bound, 0,
-                                            kKeyBits + 1, h->stream));
+  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
+                                             h->nvals_in.p, h->svals.p, (size_t)T_bound, 0,
+                                             kKeyBits + 1, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
                      h->cfg.p, h->svals.p, h->stree.p, h->stree32.p);
@@ -1037,10 +1042,11 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
                      h->ckeys_in.p, h->cvals_in.p);
   HIPCHK(hipGetLastError());
+  // candidates only need locality (the scan order never changes a result): top 16 key bits
   tb = h->sort_tmp.n;
-  HIPCHK(hipcub::DeviceRadixSort::SortPairs(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
-                                            h->cvals_in.p, h->cperm.p, nb, 0, kKeyBits + 1,
-                                            h->stream));
+  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
+                                             h->cvals_in.p, h->cperm.p, (size_t)nb,
+                                             kKeyBits + 1 - 16, kKeyBits + 1, h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
                      h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
@@ -1543,10 +1549,12 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->cperm.ensure(B);
   if (!rc) {
     size_t t1 = 0, t2 = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t1, h->nkeys_in.p, h->skeys.p, h->nvals_in.p,
-                                              h->svals.p, (int)N, 0, 64, h->stream));
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, t2, h->ckeys_in.p, h->ckeys.p, h->cvals_in.p,
-                                              h->cperm.p, (int)B, 0, 64, h->stream));
+    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t1, h->nkeys_in.p, h->skeys.p,
+                                               h->nvals_in.p, h->svals.p, (size_t)N, 0, 64,
+                                               h->stream));
+    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t2, h->ckeys_in.p, h->ckeys.p,
+                                               h->cvals_in.p, h->cperm.p, (size_t)B, 0, 64,
+                                               h->stream));
     size_t t3 = 0;
     HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, h->cflag.p, h->cid.p, (int)N, h->stream));
     rc = h->sort_tmp.ensure(std::max(std::max(t1, t2), t3));
