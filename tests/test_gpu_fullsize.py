@@ -1,0 +1,102 @@
+"""GPU parity at BASELINE.json's full sizes (configs[1] C2 and configs[2] C3).
+
+C2 (4 boxes, 2 kg, nov, 1e5 batched samples) is small enough for the oracle's batched
+restatement: node count, extend-step count, goal node and trajectory are compared directly.
+C3 (16 boxes, 5 kg, rne, 1e6 samples) is checked through size-independent properties:
+determinism, tree invariants (parents precede children, cost = parent cost + distance,
+exactly as rrt_star.py:18-63 maintains them), every sampled tree node is a valid
+configuration for the oracle (limits, collision, torque), the goal node is within the goal
+tolerance and the returned trajectory passes the oracle's dynamic torque test.
+"""
+import numpy as np
+import pytest
+
+import oracle as O  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+
+START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from torque_constrained_motion_planning_amd import _lib
+    return _lib.engine(0)
+
+
+def _query(seed, n_obs, mode, mass):
+    """SURVEY 8d query: start/goal collision-free and torque-feasible, straight edge blocked
+    (so the tree has to grow)."""
+    from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene
+    rng = np.random.default_rng(seed)
+    while True:
+        goal = LO + (HI - LO) * rng.random(7)
+        obs = obstacle_array(random_box_scene(rng, n_obs))
+        if O.collision(START, obs) or O.collision(goal, obs):
+            continue
+        if not (O.torque_ok(goal, mode, mass) and O.torque_ok(START, mode, mass)):
+            continue
+        nsafe, nsteps, _ = O.check_edge(START, goal, obs, mode, mass, cull=2)
+        if nsafe == nsteps:
+            continue
+        return obs, goal
+
+
+def _dist(a, b):
+    d = b - a
+    return np.sqrt((10.0 * (d * d)).sum(axis=-1))
+
+
+def test_c2_full_size_vs_oracle(eng):
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    obs, goal = _query(21, 4, 1, 2.0)
+    (path, vels, accels, psg), r, raw = rrt_star_batched(
+        START, goal, obs, 1, 2.0, 5.0, 100_000, batch=65536, seed=77, engine=eng)
+    ref = O.rrt_run(START, goal, 100_000, obs, 1, 2.0, 5.0, batch=65536, seed=77, cull=2)
+    assert r.n_nodes == ref["n_nodes"]
+    assert r.edge_steps == ref["edge_steps"]
+    assert r.goal_node == ref["goal_node"]
+    assert r.status == ref["status"]
+    if ref["status"] in (0, 3):
+        assert np.abs(raw["waypoints"] - ref["waypoints"]).max() < 1e-12
+        assert np.abs(raw["q"] - ref["q"]).max() < 1e-9
+        assert np.abs(raw["qd"] - ref["qd"]).max() < 1e-9
+        assert np.abs(raw["qdd"] - ref["qdd"]).max() < 1e-9
+
+
+def test_c3_full_size_properties(eng):
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    obs, goal = _query(1234, 16, 2, 5.0)
+    args = (START, goal, obs, 2, 5.0, 5.0, 1_000_000)
+    (path, vels, accels, psg), r, raw = rrt_star_batched(*args, batch=262144, seed=5,
+                                                         engine=eng)
+    cfg, cost, par, n = eng.plan_tree(r.n_nodes)
+    assert n == r.n_nodes and 1 < n <= 1_000_001
+    # determinism of the batched frontier
+    (_, _, _, _), r2, raw2 = rrt_star_batched(*args, batch=262144, seed=5, engine=eng)
+    assert (r2.n_nodes, r2.edge_steps, r2.goal_node) == (r.n_nodes, r.edge_steps, r.goal_node)
+    # tree invariants: root first, parents inserted before children, costs consistent
+    assert np.allclose(cfg[0], START) and cost[0] == 0.0
+    idx = np.arange(1, n)
+    assert np.all(par[1:] >= 0) and np.all(par[1:] < idx)
+    d = _dist(cfg[par[1:]], cfg[1:])
+    assert np.allclose(cost[1:], cost[par[1:]] + d, rtol=1e-12, atol=1e-12)
+    # every node is a valid configuration (limits, collision, search-time torque)
+    rng = np.random.default_rng(0)
+    pick = rng.choice(n, size=min(n, 3000), replace=False)
+    for i in pick:
+        assert not O.collision(cfg[i], obs)
+        assert O.torque_ok(cfg[i], 2, 5.0)
+    if r.goal_found:
+        g = cfg[r.goal_node]
+        assert _dist(g, goal) < 1e-2
+        wp = raw["waypoints"]
+        assert np.allclose(wp[0], START) and np.array_equal(wp[-1], g)
+        if r.status == 0:
+            # the returned trajectory passes the reference's dynamic torque test
+            q, qd, qdd = raw["q"], raw["qd"], raw["qdd"]
+            sel = np.arange(0, len(q), max(1, len(q) // 500))
+            for i in sel:
+                assert O.torque_ok(q[i], 2, 5.0, qd=qd[i], qdd=qdd[i])
