@@ -133,3 +133,31 @@ def test_shard_deal_covers_c4():
         ids = [shard.queries_for_rank(64, world, r) for r in range(world)]
         assert sorted(sum(ids, [])) == list(range(64))
         assert max(map(len, ids)) - min(map(len, ids)) <= 1
+
+
+def test_trajectory_npz_and_meta_csv(tmp_path):
+    """collect_data.py:108-131,146-159 output format: keys, shapes, CSV header."""
+    import csv
+    from torque_constrained_motion_planning_amd import traj_io
+    rng = np.random.default_rng(3)
+    K = 17
+    q, qd, qdd, tau = (rng.normal(size=(K, 7)) for _ in range(4))
+    dts = rng.random(K)
+    robot = SC.PandaRobot()
+    confs = [U.Conf(robot, list(range(7)), q[i], velocities=list(qd[i]),
+                    accelerations=list(qdd[i]), dt=dts[i], torques=tau[i]) for i in range(K)]
+    traj = U.Trajectory(confs, bodies=[])
+    path = traj_io.save_traj_data(traj, str(tmp_path), "rne_run_0.npz")
+    z = traj_io.load_traj_data(path)
+    assert set(z) == {"q", "qd", "qdd", "torques", "ts"}
+    assert np.array_equal(z["q"], q) and np.array_equal(z["qd"], qd)
+    assert np.array_equal(z["qdd"], qdd) and np.array_equal(z["torques"], tau)
+    assert np.array_equal(z["ts"], dts)
+    assert traj_io.save_traj_data(None, str(tmp_path), "x.npz") is None
+    meta = traj_io.MetaWriter(str(tmp_path / "run_meta.csv"))
+    meta.write(1.25, 5, 0.5, True, "rne_run_0.npz")
+    meta.write(0.5, 5, 0.5, False, "nov_run_0.npz")
+    rows = list(csv.reader(open(tmp_path / "run_meta.csv")))
+    assert rows[0] == ["planning_time", "mass", "distance", "success", "filename"]
+    assert rows[1] == ["1.25", "5", "0.5", "True", "rne_run_0.npz"]
+    assert rows[2][3] == "False"
