@@ -24,6 +24,8 @@ typedef struct tcmp_handle tcmp_handle;
 #define TCMP_TORQUE_BASE 0 /* get_torque_limits_not_exceded_test_base   panda_primitives.py:13 */
 #define TCMP_TORQUE_NOV 1  /* get_torque_limits_not_exceded_test_v3_nov panda_primitives.py:118 */
 #define TCMP_TORQUE_RNE 2  /* get_torque_limits_not_exceded_test_v4     panda_primitives.py:155 */
+#define TCMP_TORQUE_DYN 3  /* get_torque_limits_not_exceded_test_v2     panda_primitives.py:60
+                              (M, C, g from rne.py's model: the reference's pdm is not shipped) */
 
 /* plan status codes (tcmp_plan_result.status) */
 #define TCMP_PLAN_OK 0            /* path found and validated (rrt_star.py:211) */

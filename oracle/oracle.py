@@ -50,6 +50,7 @@ def lib():
         L.orc_rne.argtypes = [_dp, _dp, _dp, ctypes.c_double, _dp]
         L.orc_rne_batch.argtypes = [_dp, _dp, _dp, ctypes.c_long, ctypes.c_double, _dp]
         L.orc_torque_ok.argtypes = [_dp, _dp, _dp, ctypes.c_int, ctypes.c_double]
+        L.orc_dyn_tau.argtypes = [_dp, _dp, _dp, ctypes.c_double, _dp]
         L.orc_minjerk.argtypes = [_dp, ctypes.c_int, ctypes.c_int, _dp, _dp, _dp]
         L.orc_fk_links.argtypes = [_dp, _dp]
         L.orc_collision.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int]
@@ -83,6 +84,16 @@ def rne(q, qd, qdd, payload_mass=0.0):
     q = _arr(q, (-1, 7)); qd = _arr(qd, (-1, 7)); qdd = _arr(qdd, (-1, 7))
     tau = np.zeros_like(q)
     lib().orc_rne_batch(_d(q), _d(qd), _d(qdd), len(q), float(payload_mass), _d(tau))
+    return tau
+
+
+def dyn_tau(q, qd=None, qdd=None, mass=0.0):
+    """dyn-mode joint torques (panda_primitives.py:60-116 restated, see tcmp_oracle.c)."""
+    q = _arr(q, (7,))
+    qd = np.zeros(7) if qd is None else _arr(qd, (7,))
+    qdd = np.zeros(7) if qdd is None else _arr(qdd, (7,))
+    tau = np.zeros(7)
+    lib().orc_dyn_tau(_d(q), _d(qd), _d(qdd), float(mass), _d(tau))
     return tau
 
 

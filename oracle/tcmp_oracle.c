@@ -263,9 +263,46 @@ ORC_API void orc_rne_batch(const double* q, const double* qd, const double* qdd,
  * 1 = nov (:118-153: RNE with v = a = 0 always); 2 = rne (:155-193: RNE with the given
  * v/a, zeros when None).  Payload added iff mass > 0.01 (:142-144, :178-180).
  * Joint 7 never checked and equality fails: range(len(max_limits)-1), `>=` (:182-183). */
+ORC_API void orc_fk_links(const double* q, double* out);
+
+/* dyn (panda_primitives.py:60-116, _v2): tau = M qdd + C qd + g + J^T [0, 0, m g, 0, 0, 0].
+ * M, C, g: the reference calls panda_dynamics_model (pdm), which it does not ship; restated
+ * with rne.py's model without payload (PARITY UNPINNED against pdm).  J: pybullet
+ * calculateJacobian at panda_grasptarget (compute_jacobian, utils.py), whose linear z row is
+ * (z_i x (p_target - o_i))_z for revolute joint i with axis z_i through the frame origin o_i;
+ * the two finger columns are dropped by torques[:7].  Payload mass enters only through the
+ * force term, without the 0.01 kg threshold of the other tests. */
+static void orc_dyn_torques(const double* q, const double* qd, const double* qdd, double mass,
+                            double tau[7]) {
+  double fr[120];
+  orc_rne(q, qd, qdd, 0.0, tau);
+  orc_fk_links(q, fr);
+  const double* H = fr + 12 * 7; /* hand frame: grasp target = hand + 0.105 z (urdf :87-91) */
+  double pe[3];
+  for (int k = 0; k < 3; ++k) pe[k] = H[9 + k] + H[3 * k + 2] * 0.105;
+  for (int i = 0; i < 7; ++i) {
+    const double* F = fr + 12 * i;
+    const double zx = F[2], zy = F[5];
+    const double rx = pe[0] - F[9], ry = pe[1] - F[10];
+    tau[i] += mass * 9.81 * (zx * ry - zy * rx);
+  }
+}
+
+ORC_API void orc_dyn_tau(const double* q, const double* qd, const double* qdd, double mass,
+                         double* tau) {
+  orc_dyn_torques(q, qd, qdd, mass, tau);
+}
+
 ORC_API int orc_torque_ok(const double* q, const double* qd, const double* qdd, int mode,
                           double mass) {
   if (mode == 0) return 1;
+  if (mode == 3) {
+    double z[7] = {0}, tau[7];
+    orc_dyn_torques(q, qd ? qd : z, qdd ? qdd : z, mass, tau);
+    for (int i = 0; i < 6; ++i)
+      if (fabs(tau[i]) >= ORC_EFFORT[i]) return 0;
+    return 1;
+  }
   double z[7] = {0}, tau[7];
   const double* v = (mode == 2 && qd) ? qd : z;
   const double* a = (mode == 2 && qdd) ? qdd : z;

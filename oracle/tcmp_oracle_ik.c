@@ -74,7 +74,7 @@ static double wrap_pi(double a) {
  * 4*(q4 branch) + 2*(q6 branch) + (q2 sign); valid[b] = 1 when the branch exists.
  * Returns the number of valid branches. */
 ORC_API int orc_ik8(const double* R9, const double* p3, double q7, double* sols, int* valid) {
-  const double a = 0.0825, b = 0.384, d = 0.316, d1 = 0.333, a7 = 0.088, d8 = 0.107;
+  const double a = 0.0825, b = 0.384, d = 0.316, d1 = 0.333, d8 = 0.107;
   double R8[3][3];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) R8[i][j] = R9[3 * i + j];

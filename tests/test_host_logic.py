@@ -53,10 +53,7 @@ def test_problem_and_torque_test_selection():
     p = U.Problem(robot, [], SC.Payload(5.0), 5.0, 5.0)  # default torque_test "arne"
     with pytest.raises(UnboundLocalError):
         PP.select_torque_test(p)
-    p.torque_test = "dyn"
-    with pytest.raises(NotImplementedError):
-        PP.select_torque_test(p)
-    for name, mode in (("base", 0), ("nov", 1), ("rne", 2)):
+    for name, mode in (("base", 0), ("nov", 1), ("rne", 2), ("dyn", 3)):
         p.torque_test = name
         assert PP.select_torque_test(p).mode == mode
     # nov: payload None -> mass 0 (panda_primitives.py:134-135)
@@ -65,6 +62,10 @@ def test_problem_and_torque_test_selection():
     # rne: ptotalMass default bound at creation (:171), payload_mass None -> get_mass
     p3 = U.Problem(robot, [], SC.Payload(2.5), None, 5.0, "rne")
     assert PP.select_torque_test(p3).payload_mass == 2.5
+    # dyn: mass as nov (panda_primitives.py:71-75), ptotalMass ignored
+    p4 = U.Problem(robot, [], SC.Payload(3.0), None, 5.0, "dyn")
+    assert PP.select_torque_test(p4).payload_mass == 3.0
+    assert PP.select_torque_test(U.Problem(robot, [], None, 7.0, 5.0, "dyn")).payload_mass == 0.0
 
 
 def test_obstacle_packing():

@@ -101,3 +101,32 @@ def test_fk_matches_survey_check():
     z7 = link7[:9].reshape(3, 3)[:, 2]
     p8 = link7[9:] + 0.107 * z7
     assert np.abs(p8 - [0.30689, 0.0, 0.59028]).max() < 5e-5
+
+
+def test_dyn_tau_jacobian_term():
+    """dyn mode (panda_primitives.py:60-116): tau = rne(q, qd, qdd, 0) + J^T [0,0,m g,0,0,0].
+    The force term is checked against a finite-difference Jacobian of the grasp-target height
+    (hand frame + 0.105 z, the URDF's panda_grasptarget) through the oracle FK.  M, C, g are
+    rne.py's; pdm itself is absent from the reference, so this is parity unpinned against it."""
+    rng = np.random.default_rng(2)
+    lo = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+    hi = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+
+    def target_z(q):
+        F = O.fk_links(q)[7]
+        return F[11] + 0.105 * F[8]
+
+    for _ in range(20):
+        q = lo + (hi - lo) * rng.random(7)
+        qd = rng.uniform(-2, 2, 7)
+        qdd = rng.uniform(-5, 5, 7)
+        base = O.dyn_tau(q, qd, qdd, 0.0)
+        assert np.abs(base - O.rne(q, qd, qdd, 0.0)[0]).max() < 1e-12
+        m = 3.5
+        ext = O.dyn_tau(q, qd, qdd, m) - base
+        h = 1e-6
+        J = np.array([(target_z(q + h * e) - target_z(q - h * e)) / (2 * h) for e in np.eye(7)])
+        assert np.abs(ext - m * 9.81 * J).max() < 1e-6
+        ok = O.torque_ok(q, 3, m, qd, qdd)
+        eff = np.array([87, 87, 87, 87, 12, 12, 12.0])
+        assert ok == bool((np.abs(base + ext)[:6] < eff[:6]).all())

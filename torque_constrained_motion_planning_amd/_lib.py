@@ -17,7 +17,7 @@ _i32p = ctypes.POINTER(ctypes.c_int32)
 _i64p = ctypes.POINTER(ctypes.c_int64)
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 
-TORQUE_BASE, TORQUE_NOV, TORQUE_RNE = 0, 1, 2
+TORQUE_BASE, TORQUE_NOV, TORQUE_RNE, TORQUE_DYN = 0, 1, 2, 3
 PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_MINJERK_ASSERT = range(5)
 
 # C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)

@@ -676,6 +676,44 @@ __device__ __forceinline__ void frame_step(double R[9], double p[3], const doubl
   for (int k = 0; k < 3; ++k) p[k] = np[k];
 }
 
+// dyn mode (panda_primitives.py:60-116, get_torque_limits_not_exceded_test_v2):
+// tau = M qdd + C qd + g + J^T [0, 0, m g, 0, 0, 0].  The reference takes M, C, g from
+// panda_dynamics_model, which it does not ship: here they are rne.py's model without payload
+// (parity unpinned against pdm).  J is pybullet's Jacobian at panda_grasptarget; its linear z
+// row is (z_i x (p_target - o_i))_z for joint axis z_i through the URDF joint frame origin
+// o_i; the grasp target sits 0.107 + 0.105 along link7's z axis (the hand only turns about z).
+// The payload mass enters only through the force term, with no 0.01 kg threshold.
+template <bool DYN>
+__device__ __forceinline__ bool torque_ok_dyn(const double cq[7], const double sq[7],
+                                              const double qd[7], const double qdd[7],
+                                              double mass) {
+  double tau[7];
+  rne<DYN>(cq, sq, qd, qdd, 0.0, tau);
+  double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
+  double zx[7], zy[7], ox[7], oy[7];
+#pragma unroll
+  for (int j = 0; j < 7; ++j) {
+    const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
+    const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+    const double t[3] = {kJx[j], kJy[j], kJz[j]};
+    frame_step(R, p, Rl, t);
+    zx[j] = R[2];
+    zy[j] = R[5];
+    ox[j] = p[0];
+    oy[j] = p[1];
+  }
+  constexpr double kTarget = kFlangeZ + 0.105;
+  const double px = p[0] + R[2] * kTarget, py = p[1] + R[5] * kTarget;
+  const double f = mass * 9.81;
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    const double t = tau[i] + f * (zx[i] * (py - oy[i]) - zy[i] * (px - ox[i]));
+    ok &= !(fabs(t) >= kEffort[i]);
+  }
+  return ok;
+}
+
 // classify one (link, obstacle) pair with the link pose (R, p):
 // 0 free, 1 collision, 2 undecided (needs the exact test)
 __device__ __forceinline__ int classify_pair(int link, const double R[9], const double p[3],

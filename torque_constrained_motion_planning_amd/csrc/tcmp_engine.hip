@@ -398,7 +398,8 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     bool ok = active && !coll;
     if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
       const double z[7] = {0, 0, 0, 0, 0, 0, 0};
-      ok = torque_ok<false>(cq, sq, z, z, P.mass);
+      ok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
+                                            : torque_ok<false>(cq, sq, z, z, P.mass);
     }
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_torque += c1 - c0; c0 = c1; }
@@ -559,7 +560,8 @@ __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st
       bool ok = alive && !coll;
       if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
         const double z[7] = {0, 0, 0, 0, 0, 0, 0};
-        ok = torque_ok<false>(cq, sq, z, z, P.mass);
+        ok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
+                                              : torque_ok<false>(cq, sq, z, z, P.mass);
       }
       if (alive) {
         if (ok) {
@@ -711,6 +713,7 @@ __device__ __forceinline__ bool torque_test_sample(int mode, double mass, const 
     const double z[7] = {0, 0, 0, 0, 0, 0, 0};
     return torque_ok<false>(cq, sq, z, z, mass);
   }
+  if (mode == TCMP_TORQUE_DYN) return torque_ok_dyn<true>(cq, sq, qd, qdd, mass);
   return torque_ok<true>(cq, sq, qd, qdd, mass);
 }
 
@@ -1341,7 +1344,7 @@ int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const doub
                    int64_t n, int32_t torque_mode, double payload_mass, int32_t* ok) {
   if (int rc = set_dev(h)) return rc;
   if (n < 0 || (n > 0 && (!q || !ok))) return fail(-1, "bad arguments");
-  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, q, n);
   if (!rc && qd) rc = upload7(h, h->s1, qd, n);
@@ -1379,7 +1382,7 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
   if (int rc = set_dev(h)) return rc;
   if (n < 0 || n > INT_MAX || (n > 0 && (!from || !to || !n_safe || !n_steps || !last)))
     return fail(-1, "bad arguments");
-  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, from, n);
   rc = rc ? rc : upload7(h, h->s1, to, n);
@@ -1461,7 +1464,7 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
                        double* tau) {
   if (int rc = set_dev(h)) return rc;
   if (n < 0 || !first_fail || (n > 0 && (!q || !qd || !qdd))) return fail(-1, "bad arguments");
-  if (torque_mode < 0 || torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
   *first_fail = -1;
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, q, n);
@@ -1488,7 +1491,7 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
 int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
   if (int rc = set_dev(h)) return rc;
   if (!cfg || !result) return fail(-1, "null cfg/result");
-  if (cfg->torque_mode < 0 || cfg->torque_mode > 2) return fail(-1, "unknown torque mode");
+  if (cfg->torque_mode < 0 || cfg->torque_mode > 3) return fail(-1, "unknown torque mode");
   if (cfg->max_nodes < 2 || cfg->max_batch < 1) return fail(-1, "bad capacities");
   memset(result, 0, sizeof(*result));
   result->goal_node = -1;

@@ -29,9 +29,10 @@ def arm_conf(_, __):
 class TorqueTest:
     """Torque-limit test closure (panda_primitives.py:13-193).
 
-    mode: _lib.TORQUE_BASE / TORQUE_NOV / TORQUE_RNE.  Joint 7 is never checked and a torque
-    equal to its limit fails (`range(len(max_limits)-1)`, `>=`).  The payload is added iff
-    the resolved mass exceeds 0.01 kg."""
+    mode: _lib.TORQUE_BASE / TORQUE_NOV / TORQUE_RNE / TORQUE_DYN.  Joint 7 is never checked
+    and a torque equal to its limit fails (`range(len(max_limits)-1)`, `>=`).  For nov/rne the
+    payload is added iff the resolved mass exceeds 0.01 kg; dyn applies m*9.81 at the grasp
+    target through the Jacobian, with no threshold."""
 
     def __init__(self, problem, mode, default_mass=None):
         self.problem = problem
@@ -43,7 +44,7 @@ class TorqueTest:
         p = self.problem
         if self.mode == _lib.TORQUE_BASE:
             return 0.0
-        if self.mode == _lib.TORQUE_NOV:     # :131-135
+        if self.mode in (_lib.TORQUE_NOV, _lib.TORQUE_DYN):     # :131-135 / :71-75
             m = p.payload_mass
             if m is None and p.payload is not None:
                 m = get_mass(p.payload)
@@ -59,7 +60,8 @@ class TorqueTest:
         if self.mode == _lib.TORQUE_BASE:
             return True
         m = self.resolved_mass(ptotalMass)
-        if self.mode == _lib.TORQUE_RNE and velocities is not None and accelerations is not None:
+        if (self.mode in (_lib.TORQUE_RNE, _lib.TORQUE_DYN) and velocities is not None
+                and accelerations is not None):
             return bool(_lib.engine().torque_ok([poses], self.mode, m, qd=[velocities[:7]],
                                                  qdd=[accelerations[:7]])[0])
         return bool(_lib.engine().torque_ok([poses], self.mode, m)[0])
@@ -83,10 +85,13 @@ def get_torque_limits_not_exceded_test_v4(problem, mass=None):
 
 
 def get_torque_limits_not_exceded_test_v2(problem, mass=None):
-    """`dyn` mode (panda_primitives.py:60-116) needs panda_dynamics_model (M, C, g) and a
-    pybullet Jacobian; the module is absent from the reference, so its numbers are unknown."""
-    raise NotImplementedError("torque_test='dyn' requires panda_dynamics_model, which the "
-                              "reference does not ship (panda_primitives.py:6)")
+    """`dyn` mode (panda_primitives.py:60-116): tau = M qdd + C qd + g + J^T [0,0,m g,0,0,0]
+    with J the grasp-target Jacobian.  M, C, g come from panda_dynamics_model in the reference,
+    a module it does not ship (panda_primitives.py:6); here they are rne.py's model without the
+    payload, so the absolute numbers are parity unpinned against pdm.  Mass as
+    :71-75 (problem.payload_mass, else the payload body's mass, 0 without a payload;
+    ptotalMass is ignored there, and here)."""
+    return TorqueTest(problem, _lib.TORQUE_DYN)
 
 
 class DynamFn:
