@@ -26,7 +26,8 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 from torque_constrained_motion_planning_amd import _lib, shard  # noqa: E402
-from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene  # noqa: E402
+from torque_constrained_motion_planning_amd.scene import (mesh_pack, obstacle_array,  # noqa: E402
+                                                           random_box_scene, random_mesh_scene)
 
 START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])  # utils.py:45
 PEAK_FP32_TFLOPS = 157.3    # MI355X fp32 vector peak (spec, MI355X_MICROARCH.md)
@@ -54,39 +55,78 @@ def pmc_traffic(kernel):
     return (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
 
 
-def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None):
-    """Scene + goal: boxes rejected while start/goal collide; goal collision-free and
-    torque-feasible."""
+# BASELINE.json configs (SURVEY 8 sizes): boxes, meshes, torque test, payload, samples per
+# query, queries per step (all ranks together), scaling
+WORKLOADS = {
+    "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=32768,
+               queries=1, scaling="weak",
+               text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
+                    "batched samples per query, one query per GPU per step"),
+    "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
+               batch=262144, queries=1, scaling="weak",
+               text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
+                    "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
+    "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=32768,
+               queries=64, scaling="strong",
+               text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
+                    "samples each) per step, sharded round-robin over the GPUs, solved paths "
+                    "gathered to rank 0 over RCCL"),
+    "c5": dict(boxes=0, meshes=256, mode=_lib.TORQUE_RNE, mass=5.0, samples=10_000_000,
+               batch=262144, queries=1, scaling="strong",
+               text="C5: dense clutter, 256 convex meshes (Panda link hulls scaled 0.5-1.5, "
+                    "random poses), 5 kg, rne, 1e7 samples per step split over the GPUs "
+                    "(independent replica trees of 1e7/N samples, same scene)"),
+}
+
+
+def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None, n_mesh=0):
+    """Scene + goal: obstacles rejected while start/goal collide; goal collision-free and
+    torque-feasible, straight start->goal edge blocked.  Returns (boxes (n, 15),
+    MeshPack or None, goal)."""
     rng = np.random.default_rng(seed)
     eng = engine
     lo = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
     hi = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+    empty = np.zeros((0, 15))
     while True:
         goal = lo + (hi - lo) * rng.random(7)
+        eng.set_scene(empty)
+        if eng.collides(np.stack([START, goal])).any():
+            continue
         boxes = []
-        for _ in range(200):
+        for _ in range(200 if n_obs else 0):
             cand = random_box_scene(rng, 1)
-            arr = obstacle_array(boxes + cand)
-            eng.set_scene(arr)
+            eng.set_scene(obstacle_array(cand))
             if not eng.collides(np.stack([START, goal])).any():
                 boxes += cand
             if len(boxes) == n_obs:
                 break
         if len(boxes) < n_obs:
             continue
+        meshes = []
+        for _ in range(40 * n_mesh):
+            cand = random_mesh_scene(rng, 1)
+            eng.set_scene(empty, cand)
+            if not eng.collides(np.stack([START, goal])).any():
+                meshes += cand
+            if len(meshes) == n_mesh:
+                break
+        if len(meshes) < n_mesh:
+            continue
         obs = obstacle_array(boxes)
-        eng.set_scene(obs)
+        pack = mesh_pack(meshes)
+        eng.set_scene(obs, pack)
         if not (eng.torque_ok([goal], mode, mass)[0] and eng.torque_ok([START], mode, mass)[0]):
             continue
         # the straight start->goal edge must be blocked, so the tree has to grow to the goal
         ns, nt, _ = eng.check_edges([START], [goal], mode, mass)
         if ns[0] < nt[0]:
-            return obs, goal
+            return obs, pack, goal
 
 
 def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass=5.0,
-              exec_time=5.0):
-    eng.set_scene(obs)
+              exec_time=5.0, meshes=None):
+    eng.set_scene(obs, meshes)
     st = eng.plan_begin(START, goal, mode, mass, exec_time, max_nodes=n_samples + 1,
                         max_batch=batch, seed=seed)
     if st != _lib.PLAN_OK:
@@ -97,7 +137,8 @@ def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass
     return r, out
 
 
-def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0):
+def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=None,
+                 what="C3 scene (16 boxes, 5 kg, rne)"):
     """Oracle (C restatement of the reference loop, B = 1 = rrt_star.py semantics) on the
     same scene and Philox sample stream: single core in-process, then one independent query
     per host core (separate worker processes that never touch the GPU).  The all-core rate
@@ -106,13 +147,19 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0):
     import tempfile
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
+    O.set_meshes(meshes)
     t0 = time.perf_counter()
     ref = O.rrt_run(START, goal, n_samples, obs, mode, mass, 5.0, batch=1, seed=seed, cull=2)
     dt1 = time.perf_counter() - t0
     single = n_samples / dt1
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "scene.npz")
-        np.savez(path, start=START, goal=goal, obs=obs, mode=mode, mass=mass)
+        extra = {}
+        if meshes is not None:
+            extra = dict(m_verts=meshes.verts, m_vert_off=meshes.vert_off, m_planes=meshes.planes,
+                         m_plane_off=meshes.plane_off, m_edges=meshes.edges,
+                         m_edge_off=meshes.edge_off, m_boxes=meshes.boxes)
+        np.savez(path, start=START, goal=goal, obs=obs, mode=mode, mass=mass, **extra)
         worker = os.path.join(REPO, "oracle", "bench_worker.py")
         t0 = time.perf_counter()
         procs = [subprocess.Popen([sys.executable, worker, path, str(n_samples), str(seed + 1 + i)],
@@ -126,9 +173,9 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0):
             "cores": len(done) if multi else 1, "kind": "port",
             "single_core": single,
             "sample": "oracle/tcmp_oracle.c sequential RRT* (B=1, reference loop semantics) on the "
-                      "same C3 scene (16 boxes, 5 kg, rne): %d samples per query; single core "
+                      "same %s: %d samples per query; single core "
                       "%.1f s (%d nodes, %d extend steps); %d independent queries, one per core, "
-                      "%.1f s wall" % (n_samples, dt1, ref["n_nodes"], ref["edge_steps"],
+                      "%.1f s wall" % (what, n_samples, dt1, ref["n_nodes"], ref["edge_steps"],
                                        len(done), dtw)}
 
 
@@ -137,9 +184,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--samples", type=int, default=1_000_000)
-    ap.add_argument("--batch", type=int, default=262144)
-    ap.add_argument("--obstacles", type=int, default=16)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
+                    help="BASELINE.json config (default c3, the headline metric's config)")
+    ap.add_argument("--samples", type=int, default=None, help="samples per query")
+    ap.add_argument("--batch", type=int, default=None)
+    ap.add_argument("--obstacles", type=int, default=None, help="boxes per scene")
     ap.add_argument("--cpu-samples", type=int, default=40000)
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
                     help="host cores for the multi-core CPU baseline (16 = one GPU's share)")
@@ -158,9 +207,28 @@ def main():
         tdist.init_process_group("nccl")
         dist = tdist
 
+    W = dict(WORKLOADS[args.workload])
+    if args.samples is not None:
+        W["samples"] = args.samples
+    if args.batch is not None:
+        W["batch"] = args.batch
+    if args.obstacles is not None:
+        W["boxes"] = args.obstacles
+    if args.workload == "c5":
+        W["samples"] = W["samples"] // world  # 1e7 per step over all GPUs
+    mode, mass = W["mode"], W["mass"]
+    n_obs_total = W["boxes"] + W["meshes"]
+
     eng = _lib.Engine(local_rank)
-    # one scene per rank (query id = rank); the goal is fixed per rank, seeds vary per step
-    obs, goal = make_query(1234 + rank, n_obs=args.obstacles, engine=eng)
+    # query ids of this rank: c4 shards 64 queries round-robin, the others run one per rank;
+    # scene and goal are fixed per query id, sample seeds vary per step.  c5: one scene for all
+    # ranks (query id 0), independent replica trees.
+    if W["queries"] > 1:
+        qids = shard.queries_for_rank(W["queries"], world, rank)
+    else:
+        qids = [0 if args.workload == "c5" else rank]
+    queries = [make_query(1234 + q, n_obs=W["boxes"], mode=mode, mass=mass, engine=eng,
+                          n_mesh=W["meshes"]) for q in qids]
 
     def barrier():
         if dist is not None:
@@ -168,25 +236,29 @@ def main():
             torch.cuda.synchronize()
             dist.barrier()
 
-    def gather(out, qid):
-        # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
-        if dist is None:
-            return
-        shard.gather_trajectories(dist, [shard.pack_trajectory(out)], [qid], world, rank,
-                                  device="cuda")
-
     step_seed = lambda s: 1234 + rank * 100003 + s  # noqa: E731
+
+    def step(s):
+        outs, res = [], []
+        for j, (obs, pack, goal) in enumerate(queries):
+            r, out = run_query(eng, obs, goal, W["samples"], W["batch"], step_seed(s) + 7919 * j,
+                               mode, mass, meshes=pack)
+            outs.append(out)
+            res.append(r.as_dict())
+        if dist is not None:
+            # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
+            shard.gather_trajectories(dist, [shard.pack_trajectory(o) for o in outs],
+                                      list(qids), world, rank, device="cuda")
+        return res
+
     for w in range(args.warmup):
-        r, out = run_query(eng, obs, goal, args.samples, args.batch, step_seed(10_000 + w))
-        gather(out, w)
+        step(10_000 + w)
 
     barrier()
     t0 = time.perf_counter()
     results = []
     for s in range(args.steps):
-        r, out = run_query(eng, obs, goal, args.samples, args.batch, step_seed(s))
-        gather(out, s * world + rank)
-        results.append(r.as_dict())
+        results += step(s)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -195,7 +267,8 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
-    total_samples = args.samples * args.steps * world
+    n_queries_total = W["queries"] if W["queries"] > 1 else world
+    total_samples = W["samples"] * n_queries_total * args.steps
     S = args.steps
     kernel_ms = {k: sum(x[k] for x in results) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
@@ -222,7 +295,8 @@ def main():
     # survives the cull (device counters), fp64 VALU
     steps = sum(x["edge_steps"] for x in results)
     sat = sum(x["pairs_sat"] for x in results)
-    edge_flop = steps * (F_FK + F_BP * N_LINKS * args.obstacles + F_RNE_STATIC) + F_SAT * sat
+    f_rne = 0 if mode == _lib.TORQUE_BASE else F_RNE_STATIC
+    edge_flop = steps * (F_FK + F_BP * N_LINKS * n_obs_total + f_rne) + F_SAT * sat
     ed_ms = sum(x["ms_edges"] for x in results)
     ed_tf = edge_flop / (ed_ms * 1e-3) / 1e12 if ed_ms > 0 else 0.0
     roof_ed = {
@@ -231,13 +305,13 @@ def main():
         "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges"),
         "algorithmic": "per extend step F_fk %d + F_bp %d x %d links x %d obstacles + F_rne %d, "
                        "+ F_sat %d per pair past the cull; %d steps, %d such pairs, %d launches" % (
-                           F_FK, F_BP, N_LINKS, args.obstacles, F_RNE_STATIC, F_SAT, steps, sat,
+                           F_FK, F_BP, N_LINKS, n_obs_total, f_rne, F_SAT, steps, sat,
                            launches)}
     dominant, other = (roof_nn, roof_ed) if nn_ms >= ed_ms else (roof_ed, roof_nn)
     # north-star HBM figure: compulsory bytes per query = 68 T_r per round (tree read
     # once) + 72 B_r per round (candidates written) + trajectory rows, over the step time
     snap = sum(x["snap_sum"] for x in results)
-    hbm_bytes = 68 * snap + 72 * total_samples / world + 22 * 8 * sum(x["n_traj"] for x in results)
+    hbm_bytes = 68 * snap + 72 * W["samples"] * len(results) + 22 * 8 * sum(x["n_traj"] for x in results)
     hbm_gbs = hbm_bytes / (dt / 1.0) / 1e9 * world if dt > 0 else 0.0
 
     line = {
@@ -249,14 +323,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": W["scaling"],
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (SURVEY 8d box scene, Philox4x32-10 samples)",
-        "config": {"workload": "C3: Panda 7-DOF, %d axis-aligned boxes, 5 kg payload, torque_test=rne "
-                               "+ min-jerk v/a validation, %d samples per query, one query per "
-                               "GPU per step" % (args.obstacles, args.samples),
-                   "batch_per_round": args.batch, "execution_time_s": 5.0,
+        "data": "synthetic (SURVEY 8d %s scene, Philox4x32-10 samples)" % (
+            "convex-mesh" if W["meshes"] else "box"),
+        "config": {"workload": W["text"], "boxes": W["boxes"], "meshes": W["meshes"],
+                   "samples_per_query": W["samples"], "queries_per_step": n_queries_total,
+                   "batch_per_round": W["batch"], "execution_time_s": 5.0,
                    "parallelism": "query-sharded x%d" % world},
         "roofline": dominant,
         "roofline_other": other,
@@ -270,8 +344,11 @@ def main():
                                                         "pairs_exact")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(obs, goal, args.cpu_samples, step_seed(0),
-                                            args.cpu_workers)
+        obs, pack, goal = queries[0]
+        cpu_n = args.cpu_samples if not W["meshes"] else max(1000, args.cpu_samples // 10)
+        line["cpu_baseline"] = cpu_baseline(obs, goal, cpu_n, step_seed(0), args.cpu_workers,
+                                            mode, mass, meshes=pack,
+                                            what=W["text"].split(",")[0] + " scene")
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -21,6 +21,16 @@ import oracle as O  # noqa: E402
 def main():
     z = np.load(sys.argv[1])
     n, seed = int(sys.argv[2]), int(sys.argv[3])
+    if "m_verts" in z:
+        class Pack:  # the MeshPack fields the oracle reads
+            def __init__(self):
+                for k in ("verts", "vert_off", "planes", "plane_off", "edges", "edge_off", "boxes"):
+                    setattr(self, k, z["m_" + k])
+                self.n = len(self.boxes)
+
+            def __len__(self):
+                return self.n
+        O.set_meshes(Pack())
     t0 = time.perf_counter()
     r = O.rrt_run(z["start"], z["goal"], n, z["obs"], int(z["mode"]), float(z["mass"]), 5.0,
                   batch=1, seed=seed, cull=2)

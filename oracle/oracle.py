@@ -61,6 +61,9 @@ def lib():
         L.orc_fk8.argtypes = [_dp, _dp, _dp]
         L.orc_ik8.argtypes = [_dp, _dp, ctypes.c_double, _dp, ctypes.POINTER(ctypes.c_int)]
         L.orc_philox_uniforms.argtypes = [ctypes.c_uint64, ctypes.c_uint64, _dp]
+        L.orc_set_meshes.argtypes = [_dp, _ip, _dp, _ip, _ip, _ip, _dp, ctypes.c_int]
+        L.orc_mesh_pair_pd.argtypes = [ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int]
+        L.orc_mesh_pair_pd.restype = ctypes.c_double
         L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
                                   ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
         assert L.orc_sizeof_cfg() == ctypes.sizeof(RrtCfg), "oracle cfg layout mismatch"
@@ -139,6 +142,38 @@ def pair_pd(link, q, box, method=0):
     3: inner box PD."""
     q = _arr(q, (7,)); b = _arr(box, (15,))
     return lib().orc_pair_pd(int(link), _d(q), _d(b), int(method))
+
+
+_mesh_keep = None
+
+
+def set_meshes(pack):
+    """Install convex-mesh obstacles (a hull.MeshPack, or None to clear) for every later
+    collision / check_edge / rrt_run call (module-level state of the oracle library)."""
+    global _mesh_keep
+    L = lib()
+    if pack is None or len(pack) == 0:
+        L.orc_set_meshes(None, None, None, None, None, None, None, 0)
+        _mesh_keep = None
+        return
+    arrs = (np.ascontiguousarray(pack.verts, dtype=np.float64),
+            np.ascontiguousarray(pack.vert_off, dtype=np.intc),
+            np.ascontiguousarray(pack.planes, dtype=np.float64),
+            np.ascontiguousarray(pack.plane_off, dtype=np.intc),
+            np.ascontiguousarray(pack.edges, dtype=np.intc),
+            np.ascontiguousarray(pack.edge_off, dtype=np.intc),
+            np.ascontiguousarray(pack.boxes, dtype=np.float64))
+    _mesh_keep = arrs
+    ip = lambda a: a.ctypes.data_as(_ip)  # noqa: E731
+    L.orc_set_meshes(_d(arrs[0]), ip(arrs[1]), _d(arrs[2]), ip(arrs[3]), ip(arrs[4]),
+                     ip(arrs[5]), _d(arrs[6]), int(pack.n))
+
+
+def mesh_pair_pd(link, q, m, method=0):
+    """Penetration depth of link hull vs installed mesh m; method 0 brute force (every
+    candidate axis), 1 Gauss-map pruned."""
+    q = _arr(q, (7,))
+    return lib().orc_mesh_pair_pd(int(link), _d(q), int(m), int(method))
 
 
 def check_edge(q1, q2, obs, torque_mode, mass, cull=1):

@@ -666,16 +666,231 @@ ORC_API double orc_pair_pd(int link, const double* q, const double* ob, int meth
   return orc_hull_box_pd_local(link, cl, A, ob + 12);
 }
 
+/* ------------------------------------------------------------------------------------ */
+/* Collision: moving link convex hull vs convex-mesh obstacle (Bullet GEOM_MESH = convex hull */
+/* of the mesh vertices), penetration >= 0.04.  World-frame hull data set by              */
+/* orc_set_meshes (same arrays as tcmp_set_meshes; host hull construction in hull.py).     */
+/* ------------------------------------------------------------------------------------ */
+static struct {
+  int n;
+  double* v; int* voff; double* pl; int* poff; int* e; int* eoff; double* box;
+} g_mesh;
+
+ORC_API int orc_set_meshes(const double* verts, const int* vert_off, const double* planes,
+                           const int* plane_off, const int* edges, const int* edge_off,
+                           const double* boxes, int n_mesh) {
+  free(g_mesh.v); free(g_mesh.voff); free(g_mesh.pl); free(g_mesh.poff);
+  free(g_mesh.e); free(g_mesh.eoff); free(g_mesh.box);
+  memset(&g_mesh, 0, sizeof(g_mesh));
+  if (n_mesh <= 0) return 0;
+  const int V = vert_off[n_mesh], F = plane_off[n_mesh], E = edge_off[n_mesh];
+  g_mesh.v = malloc(sizeof(double) * 3 * (V + 1));
+  g_mesh.pl = malloc(sizeof(double) * 4 * (F + 1));
+  g_mesh.e = malloc(sizeof(int) * 4 * (E + 1));
+  g_mesh.box = malloc(sizeof(double) * 18 * n_mesh);
+  g_mesh.voff = malloc(sizeof(int) * (n_mesh + 1));
+  g_mesh.poff = malloc(sizeof(int) * (n_mesh + 1));
+  g_mesh.eoff = malloc(sizeof(int) * (n_mesh + 1));
+  memcpy(g_mesh.v, verts, sizeof(double) * 3 * V);
+  memcpy(g_mesh.pl, planes, sizeof(double) * 4 * F);
+  memcpy(g_mesh.e, edges, sizeof(int) * 4 * E);
+  memcpy(g_mesh.box, boxes, sizeof(double) * 18 * n_mesh);
+  memcpy(g_mesh.voff, vert_off, sizeof(int) * (n_mesh + 1));
+  memcpy(g_mesh.poff, plane_off, sizeof(int) * (n_mesh + 1));
+  memcpy(g_mesh.eoff, edge_off, sizeof(int) * (n_mesh + 1));
+  g_mesh.n = n_mesh;
+  return 0;
+}
+
+ORC_API int orc_mesh_count(void) { return g_mesh.n; }
+
+/* the link's hull in the world frame (frame fr = R(9) p(3)) */
+typedef struct { int nv, nf, ne; double v[160 * 3]; double pl[320 * 4]; int e[480 * 4]; } orc_whull;
+
+static void link_world_hull(int link, const double* fr, orc_whull* H) {
+  const double* R = fr;
+  const double* p = fr + 9;
+  const int v0 = tcmp_geo_vert_off[link], f0 = tcmp_geo_plane_off[link], e0 = tcmp_geo_edge_off[link];
+  H->nv = tcmp_geo_vert_off[link + 1] - v0;
+  H->nf = tcmp_geo_plane_off[link + 1] - f0;
+  H->ne = tcmp_geo_edge_off[link + 1] - e0;
+  for (int i = 0; i < H->nv; ++i) {
+    const double* a = tcmp_geo_verts + 4 * (v0 + i);
+    for (int k = 0; k < 3; ++k)
+      H->v[3 * i + k] = R[3 * k] * a[0] + R[3 * k + 1] * a[1] + R[3 * k + 2] * a[2] + p[k];
+  }
+  for (int i = 0; i < H->nf; ++i) {
+    const double* a = tcmp_geo_planes + 8 * (f0 + i);
+    double n[3];
+    for (int k = 0; k < 3; ++k) n[k] = R[3 * k] * a[0] + R[3 * k + 1] * a[1] + R[3 * k + 2] * a[2];
+    for (int k = 0; k < 3; ++k) H->pl[4 * i + k] = n[k];
+    H->pl[4 * i + 3] = a[3] + (n[0] * p[0] + n[1] * p[1] + n[2] * p[2]);
+  }
+  for (int i = 0; i < H->ne; ++i) {
+    const unsigned short* q = tcmp_geo_edge_idx + 4 * (e0 + i);
+    H->e[4 * i] = q[0] - v0; H->e[4 * i + 1] = q[1] - v0;
+    H->e[4 * i + 2] = q[2] - f0; H->e[4 * i + 3] = q[3] - f0;
+  }
+}
+
+static void proj_range(const double* v, int nv, const double n[3], double* mn, double* mx) {
+  double a = INFINITY, b = -INFINITY;
+  for (int i = 0; i < nv; ++i) {
+    const double d = n[0] * v[3 * i] + n[1] * v[3 * i + 1] + n[2] * v[3 * i + 2];
+    a = fmin(a, d);
+    b = fmax(b, d);
+  }
+  *mn = a;
+  *mx = b;
+}
+
+/* Definition: SAT over every candidate axis of two convex polytopes (facets of both, every
+ * edge pair cross product), both directions, supports from all vertices.  The minimum
+ * overlap is the penetration depth (each candidate overlap is >= it and the facet normals of
+ * the Minkowski difference are among the candidates).  O(E_A E_B (V_A + V_B)). */
+ORC_API double orc_hull_mesh_pd_brute(int link, const double* fr, int m) {
+  static orc_whull A;
+  link_world_hull(link, fr, &A);
+  const double* Bv = g_mesh.v + 3 * g_mesh.voff[m];
+  const int nvb = g_mesh.voff[m + 1] - g_mesh.voff[m];
+  const double* Bp = g_mesh.pl + 4 * g_mesh.poff[m];
+  const int nfb = g_mesh.poff[m + 1] - g_mesh.poff[m];
+  const int* Be = g_mesh.e + 4 * g_mesh.eoff[m];
+  const int neb = g_mesh.eoff[m + 1] - g_mesh.eoff[m];
+  double pd = INFINITY;
+  for (int pass = 0; pass < 2; ++pass) {
+    const double* pl = pass ? Bp : A.pl;
+    const int nf = pass ? nfb : A.nf;
+    for (int f = 0; f < nf; ++f) {
+      double amn, amx, bmn, bmx;
+      proj_range(A.v, A.nv, pl + 4 * f, &amn, &amx);
+      proj_range(Bv, nvb, pl + 4 * f, &bmn, &bmx);
+      pd = fmin(pd, fmin(amx - bmn, bmx - amn));
+    }
+  }
+  for (int i = 0; i < A.ne; ++i) {
+    const double* a0 = A.v + 3 * A.e[4 * i];
+    const double* a1 = A.v + 3 * A.e[4 * i + 1];
+    double ea[3] = {a1[0] - a0[0], a1[1] - a0[1], a1[2] - a0[2]};
+    const double la = sqrt(ea[0] * ea[0] + ea[1] * ea[1] + ea[2] * ea[2]);
+    for (int k = 0; k < 3; ++k) ea[k] /= la;
+    for (int j = 0; j < neb; ++j) {
+      const double* b0 = Bv + 3 * Be[4 * j];
+      const double* b1 = Bv + 3 * Be[4 * j + 1];
+      double eb[3] = {b1[0] - b0[0], b1[1] - b0[1], b1[2] - b0[2]};
+      const double lb = sqrt(eb[0] * eb[0] + eb[1] * eb[1] + eb[2] * eb[2]);
+      for (int k = 0; k < 3; ++k) eb[k] /= lb;
+      double n[3] = {ea[1] * eb[2] - ea[2] * eb[1], ea[2] * eb[0] - ea[0] * eb[2],
+                     ea[0] * eb[1] - ea[1] * eb[0]};
+      const double l2 = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+      if (l2 < 1e-12) continue;
+      const double il = 1.0 / sqrt(l2);
+      for (int k = 0; k < 3; ++k) n[k] *= il;
+      double amn, amx, bmn, bmx;
+      proj_range(A.v, A.nv, n, &amn, &amx);
+      proj_range(Bv, nvb, n, &bmn, &bmx);
+      pd = fmin(pd, fmin(amx - bmn, bmx - amn));
+    }
+  }
+  return pd;
+}
+
+/* Same depth over the Minkowski-difference facets only: facets of B against A's vertices,
+ * facets of A against B's vertices, and the edge pairs whose Gauss-map arcs intersect
+ * (a, b = A's adjacent facet normals; c, d = B's negated), with the support read off the
+ * edge points.  Mathematically identical to the brute force when the result is >= 0; the
+ * GPU's fp64 pass (csrc/tcmp_mesh.h exact_mesh_wave) is this computation. */
+ORC_API double orc_hull_mesh_pd_gauss(int link, const double* fr, int m) {
+  static orc_whull A;
+  link_world_hull(link, fr, &A);
+  const double* Bv = g_mesh.v + 3 * g_mesh.voff[m];
+  const int nvb = g_mesh.voff[m + 1] - g_mesh.voff[m];
+  const double* Bp = g_mesh.pl + 4 * g_mesh.poff[m];
+  const int nfb = g_mesh.poff[m + 1] - g_mesh.poff[m];
+  const int* Be = g_mesh.e + 4 * g_mesh.eoff[m];
+  const int neb = g_mesh.eoff[m + 1] - g_mesh.eoff[m];
+  double pd = INFINITY;
+  for (int f = 0; f < nfb; ++f) {
+    double amn, amx;
+    proj_range(A.v, A.nv, Bp + 4 * f, &amn, &amx);
+    pd = fmin(pd, Bp[4 * f + 3] - amn);
+  }
+  for (int f = 0; f < A.nf; ++f) {
+    double bmn, bmx;
+    proj_range(Bv, nvb, A.pl + 4 * f, &bmn, &bmx);
+    pd = fmin(pd, A.pl[4 * f + 3] - bmn);
+  }
+  for (int i = 0; i < A.ne; ++i) {
+    const double* a = A.pl + 4 * A.e[4 * i + 2];
+    const double* b = A.pl + 4 * A.e[4 * i + 3];
+    const double u[3] = {b[1] * a[2] - b[2] * a[1], b[2] * a[0] - b[0] * a[2], b[0] * a[1] - b[1] * a[0]};
+    const double* pa = A.v + 3 * A.e[4 * i];
+    const double* pa1 = A.v + 3 * A.e[4 * i + 1];
+    const double ea[3] = {pa1[0] - pa[0], pa1[1] - pa[1], pa1[2] - pa[2]};
+    for (int j = 0; j < neb; ++j) {
+      const double* n1 = Bp + 4 * Be[4 * j + 2];
+      const double* n2 = Bp + 4 * Be[4 * j + 3];
+      const double c[3] = {-n1[0], -n1[1], -n1[2]}, d[3] = {-n2[0], -n2[1], -n2[2]};
+      const double cba = c[0] * u[0] + c[1] * u[1] + c[2] * u[2];
+      const double dba = d[0] * u[0] + d[1] * u[1] + d[2] * u[2];
+      if (!(cba * dba < 0)) continue;
+      const double w[3] = {d[1] * c[2] - d[2] * c[1], d[2] * c[0] - d[0] * c[2], d[0] * c[1] - d[1] * c[0]};
+      const double adc = a[0] * w[0] + a[1] * w[1] + a[2] * w[2];
+      const double bdc = b[0] * w[0] + b[1] * w[1] + b[2] * w[2];
+      if (!(adc * bdc < 0 && cba * bdc > 0)) continue;
+      const double* pb = Bv + 3 * Be[4 * j];
+      const double* pb1 = Bv + 3 * Be[4 * j + 1];
+      const double eb[3] = {pb1[0] - pb[0], pb1[1] - pb[1], pb1[2] - pb[2]};
+      double n[3] = {ea[1] * eb[2] - ea[2] * eb[1], ea[2] * eb[0] - ea[0] * eb[2], ea[0] * eb[1] - ea[1] * eb[0]};
+      const double l2 = n[0] * n[0] + n[1] * n[1] + n[2] * n[2];
+      if (l2 < 1e-24) continue;
+      if (n[0] * (a[0] + b[0]) + n[1] * (a[1] + b[1]) + n[2] * (a[2] + b[2]) < 0) {
+        n[0] = -n[0]; n[1] = -n[1]; n[2] = -n[2];
+      }
+      pd = fmin(pd, (n[0] * (pa[0] - pb[0]) + n[1] * (pa[1] - pb[1]) + n[2] * (pa[2] - pb[2])) / sqrt(l2));
+    }
+  }
+  return pd;
+}
+
+/* link (frame fr) vs mesh m: cull = outer-box SAT (free) / inner-box SAT (collision) first;
+ * cull == 2 then runs the Gauss-map test, otherwise the brute force.  Same answer. */
+static int orc_mesh_pair_collides(int link, const double* fr, int m, int cull, long* n_exact) {
+  const double* mb = g_mesh.box + 18 * m;
+  if (cull) {
+    double cl[3], A[9];
+    box_to_link(fr, mb, cl, A);
+    const double* bx = tcmp_geo_boxes + 18 * link;
+    if (obb_obb_pd(bx, bx + 3, bx + 12, cl, A, mb + 12) < ORC_PEN) return 0;
+    if (bx[15] > 0 && mb[15] > 0 && obb_obb_pd(bx, bx + 3, bx + 15, cl, A, mb + 15) >= ORC_PEN) return 1;
+  }
+  if (n_exact) ++*n_exact;
+  if (cull == 2) return orc_hull_mesh_pd_gauss(link, fr, m) >= ORC_PEN;
+  return orc_hull_mesh_pd_brute(link, fr, m) >= ORC_PEN;
+}
+
+/* method 0 brute force, 1 Gauss-map pruned */
+ORC_API double orc_mesh_pair_pd(int link, const double* q, int m, int method) {
+  double fr[120];
+  orc_fk_links(q, fr);
+  if (method == 1) return orc_hull_mesh_pd_gauss(link, fr + 12 * link, m);
+  return orc_hull_mesh_pd_brute(link, fr + 12 * link, m);
+}
+
 /* collision_fn (utils.py:3165-3218): limits first, then every moving link x obstacle.
- * Self-collision off (utils.py:56 SELF_COLLISIONS=False), no attachments. */
+ * Self-collision off (utils.py:56 SELF_COLLISIONS=False), no attachments.  Convex meshes
+ * (orc_set_meshes) after the boxes. */
 ORC_API int orc_collision(const double* q, const double* obs, int n_obs, int cull) {
   if (orc_limits_violated(q)) return 1;
-  if (n_obs <= 0) return 0;
+  if (n_obs <= 0 && g_mesh.n <= 0) return 0;
   double fr[120];
   orc_fk_links(q, fr);
   for (int l = 0; l < TCMP_NLINKS; ++l)
     for (int o = 0; o < n_obs; ++o)
       if (orc_pair_collides(l, fr + 12 * l, obs + 15 * o, cull, 0)) return 1;
+  for (int l = 0; l < TCMP_NLINKS; ++l)
+    for (int m = 0; m < g_mesh.n; ++m)
+      if (orc_mesh_pair_collides(l, fr + 12 * l, m, cull, 0)) return 1;
   return 0;
 }
 

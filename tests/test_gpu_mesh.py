@@ -1,0 +1,151 @@
+"""GPU parity for convex-mesh obstacles (BASELINE config C5: the Panda's collision hulls
+scaled 0.5-1.5 at random poses) against the CPU oracle's hull-vs-hull penetration depth.
+
+Collision flags, safe-prefix lengths and batched RRT* trees exact; trajectories within 1e-9.
+Parity against Bullet itself is unpinned (pybullet is absent): the oracle restates the
+semantics (penetration depth >= 0.04 m between convex hulls, utils.py:2833-2880).
+"""
+import numpy as np
+import pytest
+
+import oracle as O  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from torque_constrained_motion_planning_amd import _lib
+    return _lib.engine(0)
+
+
+@pytest.fixture(autouse=True)
+def _clear_oracle_meshes():
+    yield
+    O.set_meshes(None)
+
+
+def rand_q(rng, n):
+    return LO + (HI - LO) * rng.random((n, 7))
+
+
+def mesh_scene(rng, n, avoid=()):
+    from torque_constrained_motion_planning_amd.scene import random_mesh_scene, mesh_pack
+
+    def coll(q, ms):
+        O.set_meshes(mesh_pack(ms))
+        return O.collision(q, None, cull=2)
+    ms = random_mesh_scene(rng, n, avoid=list(avoid), collides=coll if avoid else None)
+    return ms, mesh_pack(ms)
+
+
+@pytest.mark.parametrize("n_mesh", [1, 8, 32])
+def test_mesh_collision_vs_oracle(eng, n_mesh):
+    rng = np.random.default_rng(40 + n_mesh)
+    ms, pack = mesh_scene(rng, n_mesh)
+    eng.set_scene(np.zeros((0, 15)), pack)
+    O.set_meshes(pack)
+    q = rand_q(rng, 1500)
+    got = eng.collides(q)
+    ref = np.array([O.collision(x, None, cull=2) for x in q])
+    assert (got == ref).all(), np.nonzero(got != ref)
+    if n_mesh >= 8:  # the scene must exercise both answers
+        assert 0 < got.sum() < len(got)
+
+
+def test_mesh_and_boxes_vs_oracle(eng):
+    from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene
+    rng = np.random.default_rng(77)
+    ms, pack = mesh_scene(rng, 12)
+    obs = obstacle_array(random_box_scene(rng, 6))
+    eng.set_scene(obs, pack)
+    O.set_meshes(pack)
+    q = rand_q(rng, 1500)
+    got = eng.collides(q)
+    ref = np.array([O.collision(x, obs, cull=2) for x in q])
+    assert (got == ref).all()
+    # replacing the meshes keeps the boxes; clearing them leaves the box scene
+    eng.set_scene(obs, None)
+    O.set_meshes(None)
+    got = eng.collides(q[:300])
+    ref = np.array([O.collision(x, obs, cull=2) for x in q[:300]])
+    assert (got == ref).all()
+
+
+def test_mesh_pairs_near_threshold(eng):
+    """Configurations placed so that single pairs sit near the 0.04 m threshold (the fp32
+    pass defers to fp64 there): flags against the oracle's brute-force depth."""
+    from torque_constrained_motion_planning_amd.scene import ConvexMesh
+    from torque_constrained_motion_planning_amd.hull import library_shapes, pack_meshes
+    rng = np.random.default_rng(5)
+    shapes = library_shapes()
+    checked = 0
+    for trial in range(40):
+        q = rand_q(rng, 1)[0]
+        fr = O.fk_links(q)
+        link = int(rng.integers(10))
+        name = list(shapes)[trial % len(shapes)]
+        v = shapes[name]
+        # a mesh whose centre sits at a random offset from the link frame origin
+        c = fr[link, 9:] + rng.normal(0, 0.08, 3)
+        from torque_constrained_motion_planning_amd.scene import random_rotation
+        m = ConvexMesh(v - v.mean(0), rotation=random_rotation(rng), position=c,
+                       scale=float(rng.uniform(0.5, 1.5)), name=name)
+        pack = pack_meshes([m])
+        O.set_meshes(pack)
+        pd = O.mesh_pair_pd(link, q, 0, 0)
+        if abs(pd - 0.04) > 0.03:
+            continue
+        eng.set_scene(np.zeros((0, 15)), pack)
+        got = bool(eng.collides([q])[0])
+        ref = O.collision(q, None, cull=0)
+        assert got == ref, (trial, pd)
+        checked += 1
+    assert checked >= 5
+
+
+def test_mesh_edges_vs_oracle(eng):
+    rng = np.random.default_rng(9)
+    ms, pack = mesh_scene(rng, 16, avoid=[START])
+    eng.set_scene(np.zeros((0, 15)), pack)
+    O.set_meshes(pack)
+    a = np.repeat(START[None], 300, 0)
+    a[150:] = rand_q(rng, 150)
+    b = rand_q(rng, 300)
+    b[:100] = np.clip(a[:100] + rng.normal(0, 0.3, (100, 7)), LO, HI)
+    ns, nt, last = eng.check_edges(a, b, 2, 5.0)
+    for i in range(len(a)):
+        s, n, l = O.check_edge(a[i], b[i], None, 2, 5.0, cull=2)
+        assert ns[i] == s and nt[i] == n, (i, ns[i], s, nt[i], n)
+        if s:
+            assert np.array_equal(last[i], l), i
+
+
+@pytest.mark.parametrize("batch,n_mesh", [(1, 8), (64, 16), (512, 32)])
+def test_mesh_batched_frontier_vs_oracle(eng, batch, n_mesh):
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    rng = np.random.default_rng(300 + batch)
+    goal = None
+    while goal is None:
+        g = rand_q(rng, 1)[0]
+        if not O.collision(g, None) and O.torque_ok(g, 2, 5.0):
+            goal = g
+    ms, pack = mesh_scene(rng, n_mesh, avoid=[START, goal])
+    n_samples = 3 * batch + 17 if batch > 1 else 60
+    (path, vels, accels, psg), r, raw = rrt_star_batched(
+        START, goal, ms, 2, 5.0, 1.0, n_samples, batch=batch, seed=99 + batch, engine=eng)
+    O.set_meshes(pack)
+    ref = O.rrt_run(START, goal, n_samples, None, 2, 5.0, 1.0, batch=batch, seed=99 + batch,
+                    cull=2)
+    assert r.n_nodes == ref["n_nodes"]
+    assert r.edge_steps == ref["edge_steps"]
+    assert r.goal_node == ref["goal_node"]
+    assert r.status == ref["status"]
+    if ref["status"] in (0, 3):
+        assert r.n_waypoints == ref["n_waypoints"]
+        assert np.abs(raw["waypoints"] - ref["waypoints"]).max() < 1e-12
+        assert np.abs(raw["q"] - ref["q"]).max() < 1e-9

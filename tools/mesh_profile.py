@@ -1,0 +1,38 @@
+#!/usr/bin/env python3
+"""k_edges clock breakdown and mesh exact-test outcomes on the C5 workload (256 convex meshes).
+
+usage: TCMP_LIB_PATH=torque_constrained_motion_planning_amd/libtcmp_prof.so \
+       python tools/mesh_profile.py [n_samples]
+(profiling build: make -C torque_constrained_motion_planning_amd/csrc prof)
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from torque_constrained_motion_planning_amd import _lib  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+    W = bench.WORKLOADS["c5"]
+    eng = _lib.Engine(0)
+    obs, pack, goal = bench.make_query(1234, n_obs=0, n_mesh=W["meshes"], engine=eng)
+    r, _ = bench.run_query(eng, obs, goal, n, W["batch"], 1234, meshes=pack)
+    c = eng.debug_counters(20)
+    tot = max(1, c[0])
+    print(json.dumps({"samples": n, "ms_edges": r.ms_edges, "ms_nearest": r.ms_nearest,
+                      "edge_steps": r.edge_steps, "pairs_tested": r.pairs_tested,
+                      "pairs_sat": r.pairs_sat, "pairs_exact": r.pairs_exact,
+                      "clk_share": {"fetch": c[1] / tot, "collision": c[2] / tot,
+                                    "torque": c[3] / tot, "tail": c[4] / tot,
+                                    "exact_in_collision": c[5] / tot, "sincos": c[6] / tot,
+                                    "tiers123_in_collision": c[7] / tot},
+                      "mesh_exact": {"outer_box_free": c[16], "inner_box_collision": c[17],
+                                     "hull_hull_fp32": c[18], "hull_hull_fp64": c[19]}}),
+          flush=True)
+
+
+if __name__ == "__main__":
+    main()

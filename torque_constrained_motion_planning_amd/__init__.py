@@ -6,6 +6,7 @@ panda_primitives); compute runs in libtcmp.so (HIP, gfx950) through a ctypes C-A
 """
 from . import _lib  # noqa: F401
 from ._lib import Engine, TcmpError, engine, load_library  # noqa: F401
-from .scene import Box, PandaRobot, Payload, get_mass, obstacle_array  # noqa: F401
+from .scene import (Box, ConvexMesh, PandaRobot, Payload, get_mass, mesh_pack,  # noqa: F401
+                    obstacle_array)
 
 __version__ = "0.1.0"

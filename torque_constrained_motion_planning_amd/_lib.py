@@ -23,7 +23,7 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 # C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
-    "tcmp_set_scene", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk", "tcmp_debug_counters",
@@ -85,6 +85,7 @@ def load_library(path=LIB_PATH):
         L.tcmp_destroy.argtypes = [vp]
         L.tcmp_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.tcmp_set_scene.argtypes = [vp, _dp, ctypes.c_int32]
+        L.tcmp_set_meshes.argtypes = [vp, _dp, _i32p, _dp, _i32p, _i32p, _i32p, _dp, ctypes.c_int32]
         L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
                                      ctypes.c_double, _i32p]
@@ -140,6 +141,7 @@ class Engine:
         self.h = h
         self.device = device
         self._scene_key = None
+        self._mesh_key = b""
 
     def _check(self, rc):
         if rc != 0:
@@ -157,12 +159,31 @@ class Engine:
             pass
 
     # ---- scene ------------------------------------------------------------------------
-    def set_scene(self, obb):
+    def set_scene(self, obb, meshes=None):
+        """Boxes (n, 15) and, optionally, convex meshes (a hull.MeshPack or ConvexMesh list)."""
         obb = np.ascontiguousarray(np.asarray(obb, dtype=np.float64).reshape(-1, 15))
-        key = obb.tobytes()
+        if meshes is not None and not hasattr(meshes, "key"):
+            from .hull import pack_meshes
+            meshes = pack_meshes(meshes)
+        mkey = meshes.key() if meshes is not None and len(meshes) else b""
+        key = (obb.tobytes(), mkey)
         if key == self._scene_key:
             return
+        self._scene_key = None
+        if self._mesh_key != mkey and not mkey:
+            self._check(self.L.tcmp_set_meshes(self.h, None, None, None, None, None, None, None, 0))
         self._check(self.L.tcmp_set_scene(self.h, _d(obb) if len(obb) else None, len(obb)))
+        if self._mesh_key != mkey and mkey:
+            i32 = lambda a: np.ascontiguousarray(a, dtype=np.int32)  # noqa: E731
+            arrs = (np.ascontiguousarray(meshes.verts, dtype=np.float64), i32(meshes.vert_off),
+                    np.ascontiguousarray(meshes.planes, dtype=np.float64), i32(meshes.plane_off),
+                    i32(meshes.edges), i32(meshes.edge_off),
+                    np.ascontiguousarray(meshes.boxes, dtype=np.float64))
+            ip = lambda a: a.ctypes.data_as(_i32p)  # noqa: E731
+            self._check(self.L.tcmp_set_meshes(self.h, _d(arrs[0]), ip(arrs[1]), _d(arrs[2]),
+                                               ip(arrs[3]), ip(arrs[4]), ip(arrs[5]),
+                                               _d(arrs[6]), int(len(meshes))))
+        self._mesh_key = mkey
         self._scene_key = key
 
     # ---- batched physics --------------------------------------------------------------

@@ -86,13 +86,26 @@ __host__ __device__ constexpr unsigned geo_lds_bytes() {
   return TCMP_TOTAL_PLANES * 16u + TCMP_TOTAL_VERTS * 12u + TCMP_TOTAL_EDGES * 8u;
 }
 
-// obstacle record on device: c(3) B(9 row-major, columns = axes) h(3) aligned(1) pad -> 16
+// obstacle record on device: c(3) B(9 row-major, columns = axes) h(3) kind(1) -> 16.
+// kind: 1 axis-aligned box, 0 oriented box, -(1 + m) convex mesh m (c, B, h = its outer box).
 struct Scene {
   const double* __restrict__ obs;    // [n][16]
   int n_obs;
   const float* __restrict__ obs32;   // [n][8]: world-AABB centre(3), H - kPen + margin (3)
   unsigned* wq;                      // this wave's LDS pair queue (collides_wave), kQcap + 2
+  // convex-mesh obstacles (tcmp_set_meshes), world frame, global memory
+  const int* __restrict__ mrange;    // [m][8]: v0 v1 f0 f1 e0 e1 (rows of the arrays below)
+  const double* __restrict__ mib;    // [m][16]: inner box record (c, B, inner half, 0)
+  const double4* __restrict__ mv64;  // [V]: x y z 0
+  const float4* __restrict__ mv32;
+  const double4* __restrict__ mp64;  // [F]: n (unit, outward), d = max n.v
+  const float4* __restrict__ mp32;
+  const double* __restrict__ me64;   // [E][16]: c = -n1, d = -n2, dxc = unit(d x c), e, v0
+  const float* __restrict__ me32;    // [E][16]
 };
+__device__ __forceinline__ int obs_mesh(const double* ob) {
+  return ob[15] < 0.0 ? (int)(-ob[15]) - 1 : -1;
+}
 constexpr int kQcap = 128;           // queued (lane, link, obstacle) pairs per wave
 constexpr unsigned kQwaveBytes = (kQcap + 2) * 4;
 
@@ -125,7 +138,10 @@ __device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* l
   const uint2* gei = reinterpret_cast<const uint2*>(g.eidx);
   for (int i = threadIdx.x; i < TCMP_TOTAL_EDGES; i += blockDim.x) ei[i] = gei[i];
   __syncthreads();
-  so = Scene{o64, sc.n_obs, o32, wq};
+  so = sc;
+  so.obs = o64;
+  so.obs32 = o32;
+  so.wq = wq;
   go = g;
   go.planes32 = pl;
   go.verts32 = vt;
@@ -519,7 +535,7 @@ constexpr float kExactGuard = 1e-4f;
 #ifdef TCMP_PROF_EXACT
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
-__device__ unsigned long long g_exact_stats[4];
+__device__ unsigned long long g_exact_stats[8];  // [4..7]: mesh pairs (exact_pair)
 #endif
 __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g) {
@@ -642,6 +658,43 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
   return fminf(pd, wave_minf(loc));
 }
 
+}  // namespace tcmp
+#include "tcmp_mesh.h"
+namespace tcmp {
+
+// Exact penetration depth of one (link, obstacle) pair, wave-cooperative (all lanes, same
+// arguments); only its comparison with kPen is used.  Boxes: the hull-vs-box test.  Meshes:
+// the link hull against the mesh's outer box ("free" below kPen - guard, the mesh lies inside
+// it) and against its inner box ("collision" at kPen + guard and above, it lies inside the
+// mesh) -- both hull-vs-box -- then the hull-vs-hull test.  fp32 first, fp64 near kPen.
+template <bool MESH>
+__device__ __forceinline__ double exact_pair(int link, const Pose PL, const double* ob,
+                                             const Scene sc, const Geo g) {
+  const int mi = MESH ? obs_mesh(ob) : -1;
+  if (!MESH || mi < 0) {
+    const float pd32 = exact_pd_wave32(link, PL, ob, g);
+    return (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) ? (double)pd32
+                                                                      : exact_pd_wave(link, PL, ob, g);
+  }
+#ifdef TCMP_PROF_EXACT
+#define TCMP_MESH_STAT(i) if (lane_id() == 0) atomicAdd(&g_exact_stats[i], 1ull)
+#else
+#define TCMP_MESH_STAT(i)
+#endif
+  const float po = exact_pd_wave32(link, PL, ob, g);
+  if (po == po && po < (float)kPen - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
+  const double* ib = sc.mib + 16 * mi;
+  if (ib[12] > 0.0) {
+    const float pi = exact_pd_wave32(link, PL, ib, g);
+    if (pi == pi && pi > (float)kPen + kExactGuard) { TCMP_MESH_STAT(5); return (double)pi; }
+  }
+  const float pm = exact_mesh_wave32(link, PL, mi, sc, g);
+  if (pm == pm && fabsf(pm - (float)kPen) > kExactGuard) { TCMP_MESH_STAT(6); return (double)pm; }
+  TCMP_MESH_STAT(7);
+  return exact_mesh_wave(link, PL, mi, sc, g);
+#undef TCMP_MESH_STAT
+}
+
 // ------------------------------------------------------------------------------------------
 // configuration check: collision (limits + 10 links x obstacles) and torque test.
 // MUST be called by every lane of the wave (uniform control flow); `active` masks lanes.
@@ -715,14 +768,16 @@ __device__ __forceinline__ bool torque_ok_dyn(const double cq[7], const double s
 }
 
 // classify one (link, obstacle) pair with the link pose (R, p):
-// 0 free, 1 collision, 2 undecided (needs the exact test)
+// 0 free, 1 collision, 2 undecided (needs the exact test).  hin: the obstacle's inner half
+// extents (a box: its own half extents; a mesh: the box inside its hull, same centre/axes).
 __device__ __forceinline__ int classify_pair(int link, const double R[9], const double p[3],
                                              const double wc[3], const double U[9],
                                              const double aabb[3],
-                                             const double* __restrict__ ob, StepStats& st) {
+                                             const double* __restrict__ ob,
+                                             const double* __restrict__ hin, StepStats& st) {
   const double* bx = tcmp_geo_boxes + 18 * link;
   const double h0 = ob[12], h1 = ob[13], h2 = ob[14];
-  const bool aligned = ob[15] != 0.0;
+  const bool aligned = ob[15] > 0.0;
   // tier 1: link OBB extent along the obstacle axes
   double dc[3] = {wc[0] - ob[0], wc[1] - ob[1], wc[2] - ob[2]};
   if (aligned) {
@@ -756,15 +811,17 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
   const double oh[3] = {bx[12], bx[13], bx[14]};
   const double ih[3] = {bx[15], bx[16], bx[17]};
   const double hb[3] = {h0, h1, h2};
-  bool inner_all = ih[0] > 0.0;
+  const double hi[3] = {hin[0], hin[1], hin[2]};
+  bool inner_all = ih[0] > 0.0 && hi[0] > 0.0;
   constexpr double P2 = kPen * kPen;
   // link box axes
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     const double rb = hb[0] * aM[3 * i + 0] + hb[1] * aM[3 * i + 1] + hb[2] * aM[3 * i + 2];
+    const double rbi = hi[0] * aM[3 * i + 0] + hi[1] * aM[3 * i + 1] + hi[2] * aM[3 * i + 2];
     const double dist = fabs(t[i]);
     if (oh[i] + rb - dist < kPen) return 0;
-    inner_all &= (ih[i] + rb - dist >= kPen);
+    inner_all &= (ih[i] + rbi - dist >= kPen);
   }
   // obstacle axes
 #pragma unroll
@@ -773,7 +830,7 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
     const double ri = ih[0] * aM[j] + ih[1] * aM[3 + j] + ih[2] * aM[6 + j];
     const double dist = fabs(t[0] * M[j] + t[1] * M[3 + j] + t[2] * M[6 + j]);
     if (ra + hb[j] - dist < kPen) return 0;
-    inner_all &= (ri + hb[j] - dist >= kPen);
+    inner_all &= (ri + hi[j] - dist >= kPen);
   }
   // cross axes U_i x B_j, |n|^2 = 1 - M_ij^2
 #pragma unroll
@@ -787,10 +844,11 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
       const double ra = oh[i1] * aM[3 * i2 + j] + oh[i2] * aM[3 * i1 + j];
       const double ri = ih[i1] * aM[3 * i2 + j] + ih[i2] * aM[3 * i1 + j];
       const double rb = hb[j1] * aM[3 * i + j2] + hb[j2] * aM[3 * i + j1];
+      const double rbi = hi[j1] * aM[3 * i + j2] + hi[j2] * aM[3 * i + j1];
       const double dist = fabs(t[i2] * M[3 * i1 + j] - t[i1] * M[3 * i2 + j]);
       const double ov = ra + rb - dist;
       if (ov < 0 || ov * ov < P2 * n2) return 0;
-      const double oi = ri + rb - dist;
+      const double oi = ri + rbi - dist;
       inner_all &= (oi >= 0 && oi * oi >= P2 * n2);
     }
   }
@@ -857,6 +915,9 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
     aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
 }
 
+// MESH = false: a scene without convex meshes (tcmp_set_meshes count 0) -- the mesh tiers
+// are compiled out, which keeps the box-only kernels' register allocation unchanged.
+template <bool MESH>
 __device__ __forceinline__ bool collides_wave(const double q[7], const double cq[7],
                                               const double sq[7], bool active,
                                               const Scene sc, const Geo g, StepStats& st) {
@@ -891,7 +952,9 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
       if (has) {
         double wc[3], U[9], aabb[3];
         link_obb(lk, R, p, wc, U, aabb);
-        cls = classify_pair(lk, R, p, wc, U, aabb, sc.obs + 16 * o, st);
+        const double* ob = sc.obs + 16 * o;
+        const int mi = MESH ? obs_mesh(ob) : -1;
+        cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, st);
       }
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
@@ -911,10 +974,7 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
 #endif
-        const float pd32 = exact_pd_wave32(lL, PL, ob, g);
-        const double pd = (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard)
-                              ? (double)pd32
-                              : exact_pd_wave(lL, PL, ob, g);
+        const double pd = exact_pair<MESH>(lL, PL, ob, sc, g);
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif

@@ -330,6 +330,7 @@ struct EdgeJob {
 #ifndef TCMP_EDGE_MINW
 #define TCMP_EDGE_MINW 2  // min waves per SIMD the register allocation must allow
 #endif
+template <bool MESH>
 __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanParams P, Scene sc_g, Geo g_g,
                                                DevState* st) {
   extern __shared__ double tcmp_lds[];
@@ -391,7 +392,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_sincos += c1 - c0; c0 = c1; }
 #endif
-    const bool coll = collides_wave(qn, cq, sq, active, sc, g, ss);
+    const bool coll = collides_wave<MESH>(qn, cq, sq, active, sc, g, ss);
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
 #endif
@@ -491,6 +492,7 @@ __global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st,
   if (act) ncount[t] = c;
 }
 
+template <bool MESH>
 __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st, Tree tr,
                                                       const int* rwlist, const int* nbr,
                                                       const int* ncount, Scene sc_g, Geo g_g) {
@@ -556,7 +558,7 @@ __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st
       if (alive) refine_step(qq, qn, ns, i);
       double cq[7], sq[7];
       for (int k = 0; k < 7; ++k) sincos(qq[k], &sq[k], &cq[k]);
-      const bool coll = collides_wave(qq, cq, sq, alive, sc, g, ss);
+      const bool coll = collides_wave<MESH>(qq, cq, sq, alive, sc, g, ss);
       bool ok = alive && !coll;
       if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
         const double z[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -756,6 +758,7 @@ __global__ void k_traj_post(DevState* st) {
 // ------------------------------------------------------------------------------------------
 // utility kernels behind the batched C-ABI entry points
 // ------------------------------------------------------------------------------------------
+template <bool MESH>
 __global__ __launch_bounds__(256) void k_check_configs(const double* q, long long n, Scene sc_g,
                                                        Geo g_g, int* collides) {
   extern __shared__ double tcmp_lds[];
@@ -770,7 +773,7 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
   double cq[7], sq[7];
   for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
   StepStats ss = {0, 0, 0};
-  const bool c = collides_wave(x, cq, sq, act, sc, g, ss);
+  const bool c = collides_wave<MESH>(x, cq, sq, act, sc, g, ss);
   if (act) collides[i] = c ? 1 : 0;
 }
 
@@ -872,6 +875,15 @@ struct tcmp_handle {
   DBuf<float> verts32, planes32;
   DBuf<unsigned short> eidx;
   int n_obs = 0;
+  // scene on the host: boxes (tcmp_set_scene) and convex meshes (tcmp_set_meshes); the device
+  // obstacle list is the boxes followed by the meshes' outer boxes
+  std::vector<double> box15;
+  int n_box = 0, n_mesh = 0;
+  std::vector<double> mesh_v, mesh_p, mesh_box;
+  std::vector<int> mesh_e, mesh_voff, mesh_poff, mesh_eoff;
+  DBuf<int> mrange;
+  DBuf<double> mib, mv64, mp64, me64;
+  DBuf<float> mv32, mp32, me32;
   DevState* st = nullptr;
   // plan
   PlanParams P{};
@@ -916,7 +928,21 @@ struct tcmp_handle {
                reinterpret_cast<const float4*>(planes32.p),
                reinterpret_cast<const ushort4*>(eidx.p)};
   }
-  Scene scene() const { return Scene{obs.p, n_obs, obs32.p}; }
+  Scene scene() const {
+    Scene s{};
+    s.obs = obs.p;
+    s.n_obs = n_obs;
+    s.obs32 = obs32.p;
+    s.mrange = mrange.p;
+    s.mib = mib.p;
+    s.mv64 = reinterpret_cast<const double4*>(mv64.p);
+    s.mv32 = reinterpret_cast<const float4*>(mv32.p);
+    s.mp64 = reinterpret_cast<const double4*>(mp64.p);
+    s.mp32 = reinterpret_cast<const float4*>(mp32.p);
+    s.me64 = me64.p;
+    s.me32 = me32.p;
+    return s;
+  }
 
   hipEvent_t get_event() {
     if (!ev_pool.empty()) {
@@ -1085,7 +1111,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(k_edges, dim3((unsigned)blocks), dim3(256), stage_lds_bytes(h->n_obs), h->stream, J, P,
+  hipLaunchKernelGGL(h->n_mesh ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), stage_lds_bytes(h->n_obs), h->stream, J, P,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1117,15 +1143,15 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (int rc = set_dev(h)) return rc;
-  if (!out || n < 0 || n > 16) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 20) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   for (int i = 0; i < n; ++i) out[i] = s.prof[i];
 #ifdef TCMP_PROF_EXACT
-  unsigned long long ex[4];
+  unsigned long long ex[8];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
-  for (int i = 0; i < 4 && 12 + i < n; ++i) out[12 + i] = ex[i];
+  for (int i = 0; i < 8 && 12 + i < n; ++i) out[12 + i] = ex[i];
 #endif
   return 0;
 }
@@ -1172,9 +1198,10 @@ int tcmp_create(int device, tcmp_handle** out) {
     HIPCHK(hipMemcpy(h->eidx.p, tcmp_geo_edge_idx, sizeof(tcmp_geo_edge_idx), hipMemcpyHostToDevice));
     // dynamic LDS above 64 KiB per workgroup must be allowed explicitly
     const int lim = (int)stage_lds_bytes(kMaxObstacles);
-    HIPCHK(hipFuncSetAttribute((const void*)k_edges, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    HIPCHK(hipFuncSetAttribute((const void*)k_check_configs, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
-    HIPCHK(hipFuncSetAttribute((const void*)k_rewire_apply, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    for (const void* k : {(const void*)k_edges<false>, (const void*)k_edges<true>,
+                          (const void*)k_check_configs<false>, (const void*)k_check_configs<true>,
+                          (const void*)k_rewire_apply<false>, (const void*)k_rewire_apply<true>})
+      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
   }
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
@@ -1193,6 +1220,9 @@ int tcmp_destroy(tcmp_handle* h) {
   h->planes32.release();
   h->eidx.release();
   h->obs32.release();
+  h->mrange.release();
+  for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64}) b->release();
+  for (auto* b : {&h->mv32, &h->mp32, &h->me32}) b->release();
   for (auto* b : {&h->verts, &h->planes, &h->edges, &h->obs, &h->cfg, &h->tgt, &h->cand,
                   &h->last, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
                   &h->s1, &h->s2, &h->s3})
@@ -1236,15 +1266,18 @@ int tcmp_destroy(tcmp_handle* h) {
   return 0;
 }
 
-int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
-  if (int rc = set_dev(h)) return rc;
-  if (n_obs < 0 || (n_obs > 0 && !obb)) return fail(-1, "bad obstacle array");
-  if (n_obs > kMaxObstacles)
-    return fail(-1, "too many obstacles (" + std::to_string(n_obs) + " > " +
-                        std::to_string(kMaxObstacles) + ", the LDS-staged scene limit)");
-  std::vector<double> tmp((size_t)std::max(n_obs, 1) * 16, 0.0);
-  for (int o = 0; o < n_obs; ++o) {
-    const double* s = obb + 15 * o;
+}  // extern "C"
+
+namespace {
+
+// Device obstacle list = boxes then the meshes' outer boxes (records of 16 doubles, kind in
+// [15]) plus the fp32 tier-0 records (world AABB centre, half extent - kPen + margin).
+int upload_scene(tcmp_handle* h) {
+  const int n = h->n_box + h->n_mesh;
+  std::vector<double> tmp((size_t)std::max(n, 1) * 16, 0.0);
+  std::vector<float> t32((size_t)std::max(n, 1) * 8, 0.f);
+  for (int o = 0; o < h->n_box; ++o) {
+    const double* s = h->box15.data() + 15 * o;
     double* d = tmp.data() + 16 * o;
     for (int k = 0; k < 15; ++k) d[k] = s[k];
     const double* R = s + 3;
@@ -1252,18 +1285,30 @@ int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
                          R[2] == 0.0 && R[3] == 0.0 && R[5] == 0.0 && R[6] == 0.0 &&
                          R[7] == 0.0;
     d[15] = aligned ? 1.0 : 0.0;
-    if (!(s[12] >= 0 && s[13] >= 0 && s[14] >= 0)) return fail(-1, "negative half extent");
-  }
-  // tier-0 records: world AABB centre and (half extent - kPen + margin), fp32 rounded outward
-  std::vector<float> t32((size_t)std::max(n_obs, 1) * 8, 0.f);
-  for (int o = 0; o < n_obs; ++o) {
-    const double* d = tmp.data() + 16 * o;
     float* f = t32.data() + 8 * o;
     for (int i = 0; i < 3; ++i) {
       const double H = fabs(d[3 + 3 * i]) * d[12] + fabs(d[4 + 3 * i]) * d[13] +
                        fabs(d[5 + 3 * i]) * d[14];
       f[i] = (float)d[i];
       f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(d[i]) + H));
+    }
+  }
+  for (int m = 0; m < h->n_mesh; ++m) {
+    const double* b = h->mesh_box.data() + 18 * m;
+    double* d = tmp.data() + 16 * (h->n_box + m);
+    for (int k = 0; k < 15; ++k) d[k] = b[k];
+    d[15] = -(double)(m + 1);
+    double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int v = h->mesh_voff[m]; v < h->mesh_voff[m + 1]; ++v)
+      for (int i = 0; i < 3; ++i) {
+        lo[i] = std::min(lo[i], h->mesh_v[3 * v + i]);
+        hi[i] = std::max(hi[i], h->mesh_v[3 * v + i]);
+      }
+    float* f = t32.data() + 8 * (h->n_box + m);
+    for (int i = 0; i < 3; ++i) {
+      const double c = 0.5 * (lo[i] + hi[i]), H = 0.5 * (hi[i] - lo[i]);
+      f[i] = (float)c;
+      f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(c) + H));
     }
   }
   if (int rc = h->obs.ensure(tmp.size())) return rc;
@@ -1273,8 +1318,124 @@ int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
   HIPCHK(hipMemcpyAsync(h->obs32.p, t32.data(), t32.size() * sizeof(float), hipMemcpyHostToDevice,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  h->n_obs = n_obs;
+  h->n_obs = n;
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
+  if (int rc = set_dev(h)) return rc;
+  if (n_obs < 0 || (n_obs > 0 && !obb)) return fail(-1, "bad obstacle array");
+  if (n_obs + h->n_mesh > kMaxObstacles)
+    return fail(-1, "too many obstacles (" + std::to_string(n_obs + h->n_mesh) + " > " +
+                        std::to_string(kMaxObstacles) + ", the LDS-staged scene limit)");
+  for (int o = 0; o < n_obs; ++o) {
+    const double* s = obb + 15 * o;
+    if (!(s[12] >= 0 && s[13] >= 0 && s[14] >= 0)) return fail(-1, "negative half extent");
+  }
+  h->box15.assign(obb, obb + 15 * (size_t)n_obs);
+  h->n_box = n_obs;
+  return upload_scene(h);
+}
+
+int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off,
+                    const double* planes, const int32_t* plane_off, const int32_t* edges,
+                    const int32_t* edge_off, const double* boxes, int32_t n_mesh) {
+  if (int rc = set_dev(h)) return rc;
+  if (n_mesh < 0) return fail(-1, "bad mesh count");
+  if (n_mesh > 0 && (!verts || !vert_off || !planes || !plane_off || !edges || !edge_off || !boxes))
+    return fail(-1, "null mesh array");
+  if (h->n_box + n_mesh > kMaxObstacles)
+    return fail(-1, "too many obstacles (" + std::to_string(h->n_box + n_mesh) + " > " +
+                        std::to_string(kMaxObstacles) + ", the LDS-staged scene limit)");
+  const int V = n_mesh ? vert_off[n_mesh] : 0, F = n_mesh ? plane_off[n_mesh] : 0,
+            E = n_mesh ? edge_off[n_mesh] : 0;
+  if (n_mesh && (vert_off[0] != 0 || plane_off[0] != 0 || edge_off[0] != 0))
+    return fail(-1, "mesh offsets must start at 0");
+  for (int m = 0; m < n_mesh; ++m) {
+    const int nv = vert_off[m + 1] - vert_off[m], nf = plane_off[m + 1] - plane_off[m],
+              ne = edge_off[m + 1] - edge_off[m];
+    if (nv < 4 || nf < 4 || ne < 6) return fail(-1, "mesh " + std::to_string(m) + " is not a 3-D hull");
+    for (int e = edge_off[m]; e < edge_off[m + 1]; ++e) {
+      const int* q = edges + 4 * e;
+      if (q[0] < 0 || q[0] >= nv || q[1] < 0 || q[1] >= nv || q[2] < 0 || q[2] >= nf || q[3] < 0 ||
+          q[3] >= nf)
+        return fail(-1, "mesh " + std::to_string(m) + ": edge index out of range");
+    }
+    const double* b = boxes + 18 * m;
+    for (int k = 12; k < 18; ++k)
+      if (!(b[k] >= 0)) return fail(-1, "mesh " + std::to_string(m) + ": negative box half extent");
+  }
+  h->mesh_v.assign(verts, verts + 3 * (size_t)V);
+  h->mesh_p.assign(planes, planes + 4 * (size_t)F);
+  h->mesh_e.assign(edges, edges + 4 * (size_t)E);
+  h->mesh_box.assign(boxes, boxes + 18 * (size_t)n_mesh);
+  if (n_mesh > 0) {
+    h->mesh_voff.assign(vert_off, vert_off + n_mesh + 1);
+    h->mesh_poff.assign(plane_off, plane_off + n_mesh + 1);
+    h->mesh_eoff.assign(edge_off, edge_off + n_mesh + 1);
+  } else {
+    h->mesh_voff.assign(1, 0);
+    h->mesh_poff.assign(1, 0);
+    h->mesh_eoff.assign(1, 0);
+  }
+  // device records: vertex/plane rows, Gauss-map edge records (global rows), inner boxes
+  std::vector<int> rg((size_t)std::max(n_mesh, 1) * 8, 0);
+  std::vector<double> ib((size_t)std::max(n_mesh, 1) * 16, 0.0);
+  std::vector<double> v64((size_t)std::max(V, 1) * 4, 0.0), p64((size_t)std::max(F, 1) * 4, 0.0),
+      e64((size_t)std::max(E, 1) * 16, 0.0);
+  for (int m = 0; m < n_mesh; ++m) {
+    int* r = rg.data() + 8 * m;
+    r[0] = vert_off[m]; r[1] = vert_off[m + 1];
+    r[2] = plane_off[m]; r[3] = plane_off[m + 1];
+    r[4] = edge_off[m]; r[5] = edge_off[m + 1];
+    const double* b = boxes + 18 * m;
+    double* d = ib.data() + 16 * m;
+    for (int k = 0; k < 12; ++k) d[k] = b[k];
+    for (int k = 0; k < 3; ++k) d[12 + k] = b[15 + k];
+    for (int e = edge_off[m]; e < edge_off[m + 1]; ++e) {
+      const int* q = edges + 4 * e;
+      const double* va = verts + 3 * (vert_off[m] + q[0]);
+      const double* vb = verts + 3 * (vert_off[m] + q[1]);
+      const double* n1 = planes + 4 * (plane_off[m] + q[2]);
+      const double* n2 = planes + 4 * (plane_off[m] + q[3]);
+      double* o = e64.data() + 16 * e;
+      // c = -n1, d = -n2 (the obstacle enters the Minkowski difference negated), d x c
+      for (int k = 0; k < 3; ++k) { o[k] = -n1[k]; o[3 + k] = -n2[k]; }
+      double w[3] = {o[4] * o[2] - o[5] * o[1], o[5] * o[0] - o[3] * o[2], o[3] * o[1] - o[4] * o[0]};
+      const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      for (int k = 0; k < 3; ++k) o[6 + k] = wl > 0 ? w[k] / wl : 0.0;
+      for (int k = 0; k < 3; ++k) { o[9 + k] = vb[k] - va[k]; o[12 + k] = va[k]; }
+    }
+  }
+  for (int v = 0; v < V; ++v)
+    for (int k = 0; k < 3; ++k) v64[4 * v + k] = verts[3 * v + k];
+  for (int f = 0; f < F; ++f)
+    for (int k = 0; k < 4; ++k) p64[4 * f + k] = planes[4 * f + k];
+  std::vector<float> v32(v64.begin(), v64.end()), p32(p64.begin(), p64.end()), e32(e64.begin(), e64.end());
+  int rc = h->mrange.ensure(rg.size());
+  rc = rc ? rc : h->mib.ensure(ib.size());
+  rc = rc ? rc : h->mv64.ensure(v64.size());
+  rc = rc ? rc : h->mp64.ensure(p64.size());
+  rc = rc ? rc : h->me64.ensure(e64.size());
+  rc = rc ? rc : h->mv32.ensure(v32.size());
+  rc = rc ? rc : h->mp32.ensure(p32.size());
+  rc = rc ? rc : h->me32.ensure(e32.size());
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mp64.p, p64.data(), p64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->me64.p, e64.data(), e64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mv32.p, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mp32.p, p32.data(), p32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->n_mesh = n_mesh;
+  return upload_scene(h);
 }
 
 int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
@@ -1367,7 +1528,7 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   int rc = upload7(h, h->s0, q, n);
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_check_configs, dim3(grid_for(n, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, h->s0.p,
+  hipLaunchKernelGGL(h->n_mesh ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, h->s0.p,
                      (long long)n, h->scene(), h->geo(), h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
@@ -1661,7 +1822,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_rewire_apply, dim3(grid_for(nb, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, P, h->st,
+  hipLaunchKernelGGL(h->n_mesh ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);

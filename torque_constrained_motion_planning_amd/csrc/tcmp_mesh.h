@@ -1,0 +1,234 @@
+// tcmp_mesh.h -- exact link-hull vs convex-mesh penetration depth (gfx950, wave-cooperative).
+//
+// Reference semantics: utils.py:2833-2880 -- Bullet closest points between the link's convex
+// hull and an obstacle's convex hull with distance = -MAX_DISTANCE; a pair collides iff the
+// penetration depth is >= 0.04 m (kPen).  Bullet is absent (parity unpinned against it); the
+// CPU oracle (oracle/tcmp_oracle.c orc_hull_mesh_pd_*) restates the same depth.
+//
+// Penetration depth of two convex polytopes = min over the facets of their Minkowski
+// difference A - B of the support h_{A-B}(n).  Those facets come from (1) facets of B,
+// (2) facets of A and (3) edge pairs (eA, eB) whose Gauss-map arcs intersect
+// (Gregorius' Minkowski-face test).  For an edge pair the support is exact from the edge
+// points themselves: n.(a0 - b0) with n = eA x eB oriented into A's normal cone.
+// Everything is evaluated in the world frame: the obstacle's hull data is stored there
+// (tcmp_set_meshes), the link's is rotated per lane.
+//
+// fp32 first pass (LDS link geometry, scalar-loaded mesh data) -> result, or NaN when an
+// axis is too close to degenerate for fp32 (nearly parallel edges, ambiguous orientation);
+// the caller re-evaluates in fp64 whenever the fp32 value is within kExactGuard of kPen or
+// NaN, so the collision decision is always the fp64 one.  A borderline Gauss-map sign in
+// fp32 can only add or drop an axis whose edge-formula value is within (angle error) x
+// (hull diameter) ~ 1e-6 m of a neighbouring exact facet axis, far inside kExactGuard.
+#pragma once
+
+namespace tcmp {
+
+__device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, int m,
+                                                   const Scene sc, const Geo g) {
+  const int lane = lane_id();
+  const int* rg = sc.mrange + 8 * m;
+  const int v0 = rg[0], v1 = rg[1], f0 = rg[2], f1 = rg[3], e0 = rg[4], e1 = rg[5];
+  const int lv0 = tcmp_geo_vert_off[link], lv1 = tcmp_geo_vert_off[link + 1];
+  const int lf0 = tcmp_geo_plane_off[link], lf1 = tcmp_geo_plane_off[link + 1];
+  const int le0 = tcmp_geo_edge_off[link], le1 = tcmp_geo_edge_off[link + 1];
+  float R[9], p[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = (float)pose.R[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = (float)pose.p[k];
+  constexpr float P = (float)kPen;
+  float loc = INFINITY;
+  // (1) mesh facets (moved into the link frame) against the link's vertices (LDS broadcast)
+  for (int base = f0; base < f1; base += 256) {
+    float nx[4], ny[4], nz[4], dd[4], mn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = base + lane + 64 * j;
+      float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
+      if (f < f1) w = sc.mp32[f];
+      nx[j] = R[0] * w.x + R[3] * w.y + R[6] * w.z;
+      ny[j] = R[1] * w.x + R[4] * w.y + R[7] * w.z;
+      nz[j] = R[2] * w.x + R[5] * w.y + R[8] * w.z;
+      dd[j] = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
+      mn[j] = INFINITY;
+    }
+    for (int v = lv0; v < lv1; ++v) {
+      const float x = g.verts32[3 * v], y = g.verts32[3 * v + 1], z = g.verts32[3 * v + 2];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
+  }
+  float pd = wave_minf(loc);
+  if (pd < P - kExactGuard) return pd;
+  // (2) link facets (moved into the world frame) against the mesh's vertices
+  for (int base = lf0; base < lf1; base += 256) {
+    float nx[4], ny[4], nz[4], dd[4], mn[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int f = base + lane + 64 * j;
+      float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
+      if (f < lf1) w = g.planes32[f];
+      nx[j] = R[0] * w.x + R[1] * w.y + R[2] * w.z;
+      ny[j] = R[3] * w.x + R[4] * w.y + R[5] * w.z;
+      nz[j] = R[6] * w.x + R[7] * w.y + R[8] * w.z;
+      dd[j] = w.w + (nx[j] * p[0] + ny[j] * p[1] + nz[j] * p[2]);
+      mn[j] = INFINITY;
+    }
+    for (int v = v0; v < v1; ++v) {
+      const float4 P4 = sc.mv32[v];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * P4.x + ny[j] * P4.y + nz[j] * P4.z);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
+  }
+  pd = fminf(pd, wave_minf(loc));
+  if (pd < P - kExactGuard) return pd;
+  // (3) edge pairs: lanes own link edges, the mesh's edges stream wave-uniformly
+  bool deg = false;
+  for (int base = le0; base < le1; base += 64) {
+    const int e = base + lane;
+    const bool valid = e < le1;
+    float ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;  // adjacent facet normals (world)
+    float ux = 0, uy = 0, uz = 0;                          // unit(b x a)
+    float ex = 0, ey = 0, ez = 0, px = 0, py = 0, pz = 0;  // edge vector, endpoint (world)
+    if (valid) {
+      const ushort4 ix = g.eidx[e];
+      const float4 na = g.planes32[ix.z], nb = g.planes32[ix.w];
+      ax = R[0] * na.x + R[1] * na.y + R[2] * na.z;
+      ay = R[3] * na.x + R[4] * na.y + R[5] * na.z;
+      az = R[6] * na.x + R[7] * na.y + R[8] * na.z;
+      bx = R[0] * nb.x + R[1] * nb.y + R[2] * nb.z;
+      by = R[3] * nb.x + R[4] * nb.y + R[5] * nb.z;
+      bz = R[6] * nb.x + R[7] * nb.y + R[8] * nb.z;
+      ux = by * az - bz * ay;
+      uy = bz * ax - bx * az;
+      uz = bx * ay - by * ax;
+      const float il = rsqrtf(ux * ux + uy * uy + uz * uz);
+      ux *= il; uy *= il; uz *= il;
+      const float x0 = g.verts32[3 * ix.x], y0 = g.verts32[3 * ix.x + 1], z0 = g.verts32[3 * ix.x + 2];
+      const float lx = g.verts32[3 * ix.y] - x0, ly = g.verts32[3 * ix.y + 1] - y0,
+                  lz = g.verts32[3 * ix.y + 2] - z0;
+      ex = R[0] * lx + R[1] * ly + R[2] * lz;
+      ey = R[3] * lx + R[4] * ly + R[5] * lz;
+      ez = R[6] * lx + R[7] * ly + R[8] * lz;
+      px = R[0] * x0 + R[1] * y0 + R[2] * z0 + p[0];
+      py = R[3] * x0 + R[4] * y0 + R[5] * z0 + p[1];
+      pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
+    }
+    const float el2 = ex * ex + ey * ey + ez * ez;
+    for (int k = e0; k < e1; ++k) {
+      const float* E = sc.me32 + 16 * k;
+      const float cx = E[0], cy = E[1], cz = E[2], dx = E[3], dy = E[4], dz = E[5];
+      const float cba = cx * ux + cy * uy + cz * uz;
+      const float dba = dx * ux + dy * uy + dz * uz;
+      if (valid && cba * dba < 0.f) {
+        const float wx = E[6], wy = E[7], wz = E[8];
+        const float adc = ax * wx + ay * wy + az * wz;
+        const float bdc = bx * wx + by * wy + bz * wz;
+        if (adc * bdc < 0.f && cba * bdc > 0.f) {
+          const float fx = E[9], fy = E[10], fz = E[11];
+          float n0 = ey * fz - ez * fy, n1 = ez * fx - ex * fz, n2 = ex * fy - ey * fx;
+          const float len2 = n0 * n0 + n1 * n1 + n2 * n2;
+          const float fl2 = fx * fx + fy * fy + fz * fz;
+          if (len2 < 1e-4f * el2 * fl2) {
+            deg = true;  // nearly parallel edges: the axis direction needs fp64
+          } else {
+            const float il = rsqrtf(len2);
+            const float ori = n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz);
+            deg |= fabsf(ori) * il < 1e-4f;
+            if (ori < 0.f) { n0 = -n0; n1 = -n1; n2 = -n2; }
+            const float ov = n0 * (px - E[12]) + n1 * (py - E[13]) + n2 * (pz - E[14]);
+            loc = fminf(loc, ov * il);
+          }
+        }
+      }
+    }
+    if (base + 64 < le1 && !__ballot(deg)) {
+      const float lf = fminf(pd, wave_minf(loc));
+      if (lf < P - kExactGuard) return lf;
+    }
+  }
+  if (__ballot(deg)) return __builtin_nanf("");
+  return fminf(pd, wave_minf(loc));
+}
+
+// fp64 restatement of exact_mesh_wave32 (same axes, strict Gauss-map test, no degeneracy
+// shortcuts): the decision-maker near kPen.  Every lane of the wave calls it.
+__device__ __noinline__ double exact_mesh_wave(int link, const Pose pose, int m, const Scene sc,
+                                               const Geo g) {
+  const int lane = lane_id();
+  const int* rg = sc.mrange + 8 * m;
+  const int v0 = rg[0], v1 = rg[1], f0 = rg[2], f1 = rg[3], e0 = rg[4], e1 = rg[5];
+  const int lv0 = tcmp_geo_vert_off[link], lv1 = tcmp_geo_vert_off[link + 1];
+  const int lf0 = tcmp_geo_plane_off[link], lf1 = tcmp_geo_plane_off[link + 1];
+  const int le0 = tcmp_geo_edge_off[link], le1 = tcmp_geo_edge_off[link + 1];
+  const double* R = pose.R;
+  const double* p = pose.p;
+  double loc = INFINITY;
+  for (int f = f0 + lane; f < f1; f += 64) {
+    const double4 w = sc.mp64[f];
+    const double nx = R[0] * w.x + R[3] * w.y + R[6] * w.z;
+    const double ny = R[1] * w.x + R[4] * w.y + R[7] * w.z;
+    const double nz = R[2] * w.x + R[5] * w.y + R[8] * w.z;
+    const double dd = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
+    double mn = INFINITY;
+    for (int v = lv0; v < lv1; ++v) {
+      const double4 P4 = *reinterpret_cast<const double4*>(g.verts + 4 * v);
+      mn = fmin(mn, nx * P4.x + ny * P4.y + nz * P4.z);
+    }
+    loc = fmin(loc, dd - mn);
+  }
+  double pd = wave_min(loc);
+  if (pd < kPen) return pd;
+  for (int f = lf0 + lane; f < lf1; f += 64) {
+    const double* W = g.planes + 8 * f;
+    const double nx = R[0] * W[0] + R[1] * W[1] + R[2] * W[2];
+    const double ny = R[3] * W[0] + R[4] * W[1] + R[5] * W[2];
+    const double nz = R[6] * W[0] + R[7] * W[1] + R[8] * W[2];
+    const double dd = W[3] + (nx * p[0] + ny * p[1] + nz * p[2]);
+    double mn = INFINITY;
+    for (int v = v0; v < v1; ++v) {
+      const double4 P4 = sc.mv64[v];
+      mn = fmin(mn, nx * P4.x + ny * P4.y + nz * P4.z);
+    }
+    loc = fmin(loc, dd - mn);
+  }
+  pd = fmin(pd, wave_min(loc));
+  if (pd < kPen) return pd;
+  for (int e = le0 + lane; e < le1; e += 64) {
+    const double* L = g.edges + 16 * e;  // e | va | n1 | n2 (link frame)
+    const double ax = R[0] * L[8] + R[1] * L[9] + R[2] * L[10];
+    const double ay = R[3] * L[8] + R[4] * L[9] + R[5] * L[10];
+    const double az = R[6] * L[8] + R[7] * L[9] + R[8] * L[10];
+    const double bx = R[0] * L[12] + R[1] * L[13] + R[2] * L[14];
+    const double by = R[3] * L[12] + R[4] * L[13] + R[5] * L[14];
+    const double bz = R[6] * L[12] + R[7] * L[13] + R[8] * L[14];
+    const double ux = by * az - bz * ay, uy = bz * ax - bx * az, uz = bx * ay - by * ax;
+    const double ex = R[0] * L[0] + R[1] * L[1] + R[2] * L[2];
+    const double ey = R[3] * L[0] + R[4] * L[1] + R[5] * L[2];
+    const double ez = R[6] * L[0] + R[7] * L[1] + R[8] * L[2];
+    const double px = R[0] * L[4] + R[1] * L[5] + R[2] * L[6] + p[0];
+    const double py = R[3] * L[4] + R[4] * L[5] + R[5] * L[6] + p[1];
+    const double pz = R[6] * L[4] + R[7] * L[5] + R[8] * L[6] + p[2];
+    for (int k = e0; k < e1; ++k) {
+      const double* E = sc.me64 + 16 * k;
+      const double cba = E[0] * ux + E[1] * uy + E[2] * uz;
+      const double dba = E[3] * ux + E[4] * uy + E[5] * uz;
+      if (!(cba * dba < 0)) continue;
+      const double adc = ax * E[6] + ay * E[7] + az * E[8];
+      const double bdc = bx * E[6] + by * E[7] + bz * E[8];
+      if (!(adc * bdc < 0 && cba * bdc > 0)) continue;
+      double n0 = ey * E[11] - ez * E[10], n1 = ez * E[9] - ex * E[11], n2 = ex * E[10] - ey * E[9];
+      const double len2 = n0 * n0 + n1 * n1 + n2 * n2;
+      if (len2 < 1e-24) continue;
+      if (n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz) < 0) { n0 = -n0; n1 = -n1; n2 = -n2; }
+      loc = fmin(loc, (n0 * (px - E[12]) + n1 * (py - E[13]) + n2 * (pz - E[14])) / sqrt(len2));
+    }
+  }
+  return fmin(pd, wave_min(loc));
+}
+
+}  // namespace tcmp

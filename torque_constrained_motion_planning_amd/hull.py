@@ -1,0 +1,167 @@
+"""Convex-mesh obstacle records (host side of tcmp_set_meshes).
+
+The reference hands Bullet a mesh file and Bullet collides the convex hull of its vertices
+(`createCollisionShape(GEOM_MESH)`, utils.py:2833-2880 closest points against it).  The
+engine needs the hull itself, so each `ConvexMesh` is reduced here, once, to:
+
+  * hull vertices (world frame)
+  * hull facet planes n.x <= d (coplanar triangles merged, unit outward n)
+  * hull edges as (va, vb, f1, f2): endpoints and the two adjacent facets (Gauss-map arcs)
+  * an outer oriented box containing the hull and an inner box inside it (same centre and
+    axes), the conservative "free" / "collision" bounds the kernels test before the exact
+    hull-vs-hull penetration depth.
+
+`pack_meshes()` concatenates the records into the flat arrays of include/tcmp.h
+(`tcmp_set_meshes`).  Mesh-local indices; row offsets per mesh.
+"""
+import numpy as np
+
+
+def hull_data(points):
+    """Convex hull of `points` -> (verts, planes[F,4] (n, dmax), edges[E,4] (va, vb, f1, f2)).
+
+    Coplanar triangles are merged into one facet (rounded to 1e-10), and edges interior to a
+    merged facet are dropped, as tools/gen_panda_geometry.py does for the robot links."""
+    from scipy.spatial import ConvexHull
+    pts = np.unique(np.asarray(points, dtype=np.float64).reshape(-1, 3), axis=0)
+    h = ConvexHull(pts)
+    keep = np.sort(h.vertices)
+    remap = -np.ones(len(pts), dtype=np.int64)
+    remap[keep] = np.arange(len(keep))
+    v = pts[keep]
+    planes, tri_plane, index = [], [], {}
+    for eq in h.equations:
+        nrm = eq[:3] / np.linalg.norm(eq[:3])
+        dmax = float((v @ nrm).max())
+        key = tuple(np.round(np.concatenate([nrm, [dmax]]), 10))
+        if key not in index:
+            index[key] = len(planes)
+            planes.append([nrm[0], nrm[1], nrm[2], dmax])
+        tri_plane.append(index[key])
+    adj = {}
+    for ti, s in enumerate(h.simplices):
+        s = remap[s]
+        for a, b in ((0, 1), (1, 2), (0, 2)):
+            adj.setdefault(tuple(sorted((int(s[a]), int(s[b])))), []).append(tri_plane[ti])
+    edges = []
+    for (a, b), fs in sorted(adj.items()):
+        if len(fs) != 2:
+            raise ValueError("non-manifold hull edge")
+        if fs[0] != fs[1]:
+            edges.append([a, b, fs[0], fs[1]])
+    return v, np.array(planes, dtype=np.float64), np.array(edges, dtype=np.int32).reshape(-1, 4)
+
+
+def fit_boxes(verts, planes, n_random=300, seed=0):
+    """Outer oriented box (contains the hull) and inner half extents (box of the same centre
+    and axes inside the hull).  PCA axes refined over random rotations for a small volume;
+    any containing box is correct, a tighter one only culls more."""
+    from scipy.spatial.transform import Rotation
+    v = np.asarray(verts, dtype=np.float64)
+    mu = v.mean(0)
+    _, _, wt = np.linalg.svd(v - mu, full_matrices=False)
+    cands = [wt.T]
+    cands += list(Rotation.random(n_random, random_state=seed).as_matrix())
+    best, best_R = np.inf, None
+    for R in cands:
+        p = v @ R
+        vol = np.prod(p.max(0) - p.min(0))
+        if vol < best:
+            best, best_R = vol, R
+    R = best_R
+    u, _, w2 = np.linalg.svd(R)
+    R = u @ w2
+    if np.linalg.det(R) < 0:
+        R[:, 2] = -R[:, 2]
+    p = v @ R
+    lo, hi = p.min(0), p.max(0)
+    half = (hi - lo) / 2 + 1e-9
+    c = R @ ((hi + lo) / 2)
+    # inner box: largest scaled copy of the outer box (same centre and axes) inside the hull
+    n, d = planes[:, :3], planes[:, 3]
+    corners = np.array([[sx, sy, sz] for sx in (-1, 1) for sy in (-1, 1) for sz in (-1, 1)])
+    ih = np.zeros(3)
+    if np.all(c @ n.T <= d - 1e-7):
+        lo_s, hi_s = 0.0, 1.0
+        for _ in range(60):
+            s = 0.5 * (lo_s + hi_s)
+            pts = c + (corners * (half * s)) @ R.T
+            if np.all(pts @ n.T <= d[None, :] - 1e-7):
+                lo_s = s
+            else:
+                hi_s = s
+        ih = half * lo_s * (1 - 1e-6)
+    return c, R, half, ih
+
+
+class ConvexMesh:
+    """A fixed convex-mesh obstacle: vertices in the mesh frame, a scale, and a world pose
+    (rotation R, translation p).  Bullet collides the hull of the vertices; so does the
+    engine."""
+
+    def __init__(self, vertices, rotation=None, position=(0.0, 0.0, 0.0), scale=1.0,
+                 name="mesh"):
+        self.vertices = np.asarray(vertices, dtype=np.float64).reshape(-1, 3)
+        self.rotation = np.eye(3) if rotation is None else np.asarray(rotation, dtype=np.float64).reshape(3, 3)
+        self.position = np.asarray(position, dtype=np.float64).reshape(3)
+        self.scale = float(scale)
+        self.name = name
+        self._rec = None
+
+    def world_vertices(self):
+        return (self.vertices * self.scale) @ self.rotation.T + self.position
+
+    def record(self):
+        """(verts, planes, edges, box18) in the world frame; cached."""
+        if self._rec is None:
+            v, pl, e = hull_data(self.world_vertices())
+            c, R, half, ih = fit_boxes(v, pl)
+            box = np.concatenate([c, R.reshape(-1), half, ih])
+            self._rec = (v, pl, e, box)
+        return self._rec
+
+    def __repr__(self):
+        return "ConvexMesh(%s, %d verts, scale %.3g)" % (self.name, len(self.vertices), self.scale)
+
+
+class MeshPack:
+    """Flat arrays of tcmp_set_meshes (include/tcmp.h)."""
+
+    def __init__(self, meshes):
+        recs = [m.record() for m in meshes]
+        self.n = len(recs)
+        self.verts = np.ascontiguousarray(np.concatenate([r[0] for r in recs]) if recs else np.zeros((0, 3)))
+        self.planes = np.ascontiguousarray(np.concatenate([r[1] for r in recs]) if recs else np.zeros((0, 4)))
+        self.edges = np.ascontiguousarray((np.concatenate([r[2] for r in recs]) if recs
+                                           else np.zeros((0, 4))).astype(np.int32))
+        self.boxes = np.ascontiguousarray(np.array([r[3] for r in recs]).reshape(-1, 18))
+        self.vert_off = np.concatenate([[0], np.cumsum([len(r[0]) for r in recs])]).astype(np.int32)
+        self.plane_off = np.concatenate([[0], np.cumsum([len(r[1]) for r in recs])]).astype(np.int32)
+        self.edge_off = np.concatenate([[0], np.cumsum([len(r[2]) for r in recs])]).astype(np.int32)
+
+    def key(self):
+        return b"".join(a.tobytes() for a in (self.verts, self.planes, self.edges, self.boxes,
+                                              self.vert_off, self.plane_off, self.edge_off))
+
+    def __len__(self):
+        return self.n
+
+
+def pack_meshes(meshes):
+    if isinstance(meshes, MeshPack):
+        return meshes
+    return MeshPack(list(meshes or []))
+
+
+def library_shapes():
+    """The Panda's collision hulls (panda_mod.urdf STL meshes, link frames), the shape
+    library SURVEY 8d names for the dense-clutter config (C5): name -> vertices."""
+    import os
+    d = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "panda_geometry.npz"))
+    off, names = d["vert_off"], [str(s) for s in d["link_names"]]
+    shapes = {}
+    for i, nm in enumerate(names):
+        if nm == "panda_rightfinger":
+            continue  # the left finger's mesh, turned about z
+        shapes[nm.replace("panda_", "")] = d["verts"][off[i]:off[i + 1]].copy()
+    return shapes

@@ -237,11 +237,11 @@ def grasp_conf_for_pose(problem, start_conf, pose, engine=None, rng=None, shuffl
     """panda_primitives.py:240-258: top grasp of problem.payload at `pose` (world_from_object,
     (point, quat) or 4x4), gripper pose, up to 25 IK attempts with the body collision check."""
     from ._lib import engine as get_engine
-    from .scene import obstacle_array
+    from .scene import mesh_pack, obstacle_array
     from .utils import get_collision_fn, get_arm_joints
 
     eng = get_engine() if engine is None else engine
-    eng.set_scene(obstacle_array(problem.fixed))
+    eng.set_scene(obstacle_array(problem.fixed), mesh_pack(problem.fixed))
     grasp = get_top_grasp(problem.payload)
     gripper_pose = multiply(from_matrix(to_matrix(pose)), invert(grasp.value))
     collision_fn = get_collision_fn(problem.robot, get_arm_joints(problem.robot), problem.fixed,

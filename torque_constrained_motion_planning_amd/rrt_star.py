@@ -182,9 +182,9 @@ def rrt_star_batched(start, goal, obstacles, torque_mode, payload_mass, executio
     """Engine-native batched frontier: n_samples Philox-drawn candidates, `batch` per round.
 
     Returns ((path, vels, accels, psg) | (None,)*4, PlanResult, raw arrays)."""
-    from .scene import obstacle_array
+    from .scene import mesh_pack, obstacle_array
     eng = engine if engine is not None else _lib.engine(device)
-    eng.set_scene(obstacle_array(obstacles))
+    eng.set_scene(obstacle_array(obstacles), mesh_pack(obstacles))
     st = eng.plan_begin(start, goal, torque_mode, payload_mass, execution_time,
                         max_nodes=int(n_samples) + 1, max_batch=int(batch), seed=seed,
                         weights=weights, resolutions=resolutions, radius=radius,

@@ -7,10 +7,14 @@ engine needs only geometry, so bodies become plain records:
   PandaRobot  -- the Panda of src/models/panda_mod.urdf (joint limits, efforts, fingers open)
   Box         -- a fixed oriented box obstacle (URDF <box> collision, e.g. table_wooden.urdf)
   Payload     -- the grasped object (mass for the torque tests, cylinder/box for grasps)
+  ConvexMesh  -- a fixed convex-mesh obstacle (URDF <mesh>; Bullet collides its hull), hull.py
 
-`obstacle_array()` packs obstacles into the C-ABI layout (15 doubles per box).
+`obstacle_array()` packs boxes into the C-ABI layout (15 doubles per box); `mesh_pack()`
+packs the convex meshes (tcmp_set_meshes).
 """
 import numpy as np
+
+from .hull import ConvexMesh, MeshPack, library_shapes, pack_meshes
 
 # panda_mod.urdf:121-285
 JOINT_LOWER = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
@@ -103,7 +107,8 @@ def get_mass(body):
 
 
 def obstacle_array(fixed):
-    """Pack Problem.fixed into the (n, 15) C-ABI layout."""
+    """Pack the boxes of Problem.fixed into the (n, 15) C-ABI layout (convex meshes are
+    packed separately by mesh_pack)."""
     if fixed is None:
         fixed = []
     if isinstance(fixed, np.ndarray):
@@ -112,6 +117,8 @@ def obstacle_array(fixed):
         return np.ascontiguousarray(fixed.astype(np.float64).reshape(-1, 15))
     rows = []
     for b in fixed:
+        if isinstance(b, ConvexMesh):
+            continue
         if isinstance(b, Box):
             rows.append(b.obb15())
         else:
@@ -145,3 +152,55 @@ def random_box_scene(rng, n, avoid=(), collides=None, aligned=True, max_tries=10
                 continue
         boxes.append(b)
     return boxes
+
+
+def mesh_pack(fixed):
+    """The ConvexMesh records of Problem.fixed as a hull.MeshPack (None when there are none)."""
+    if fixed is None or isinstance(fixed, np.ndarray):
+        return None
+    if isinstance(fixed, MeshPack):
+        return fixed
+    meshes = [b for b in fixed if isinstance(b, ConvexMesh)]
+    return pack_meshes(meshes) if meshes else None
+
+
+def random_rotation(rng):
+    """Uniform random rotation (Shoemake quaternion)."""
+    u1, u2, u3 = rng.uniform(0.0, 1.0, 3)
+    a, b = np.sqrt(1 - u1), np.sqrt(u1)
+    x, y, z, w = a * np.sin(2 * np.pi * u2), a * np.cos(2 * np.pi * u2), b * np.sin(2 * np.pi * u3), b * np.cos(2 * np.pi * u3)
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+# C5 clutter region: around the arm's reach (the SURVEY 8d box region, widened to both sides)
+MESH_REGION_LO = (-0.8, -0.8, 0.0)
+MESH_REGION_HI = (0.8, 0.8, 1.0)
+
+
+def random_mesh_scene(rng, n, avoid=(), collides=None, scale=(0.5, 1.5), lo=MESH_REGION_LO,
+                      hi=MESH_REGION_HI, keep_out=0.12, max_tries=200000):
+    """n convex meshes = the Panda's collision hulls (panda_mod.urdf STL
+    meshes) scaled U[0.5, 1.5] with uniform random orientations, centres uniform in the
+    region [lo, hi] outside a cylinder of radius keep_out around the base, rejected while any
+    configuration in `avoid` collides (collides(q, [mesh]) -> bool)."""
+    shapes = list(library_shapes().items())
+    out = []
+    tries = 0
+    while len(out) < n:
+        tries += 1
+        if tries > max_tries:
+            raise RuntimeError("could not place %d meshes" % n)
+        name, verts = shapes[int(rng.integers(len(shapes)))]
+        s = float(rng.uniform(*scale))
+        c = rng.uniform(lo, hi)
+        if np.hypot(c[0], c[1]) < keep_out:
+            continue
+        m = ConvexMesh(verts - verts.mean(0), rotation=random_rotation(rng), position=c, scale=s,
+                       name=name)
+        if collides is not None and avoid:
+            if any(collides(q, [m]) for q in avoid):
+                continue
+        out.append(m)
+    return out

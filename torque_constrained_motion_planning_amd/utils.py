@@ -9,7 +9,8 @@ import numpy as np
 
 from . import _lib
 from .scene import (ARM_JOINT_NAMES, JOINT_EFFORT, JOINT_LOWER, JOINT_UPPER, JOINT_VELOCITY,
-                    Box, Payload, PandaRobot, get_mass, obstacle_array)
+                    Box, ConvexMesh, Payload, PandaRobot, get_mass, mesh_pack,
+                    obstacle_array)
 
 PI = np.pi
 INF = float("inf")
@@ -165,12 +166,13 @@ class CollisionFn:
     def __init__(self, body, obstacles, device=0):
         self.body = body
         self.obstacles = obstacle_array(obstacles)
+        self.meshes = mesh_pack(obstacles)
         self.device = device
 
     @property
     def engine(self):
         e = _lib.engine(self.device)
-        e.set_scene(self.obstacles)
+        e.set_scene(self.obstacles, self.meshes)
         return e
 
     def __call__(self, q, verbose=False):
