@@ -42,7 +42,7 @@ int tcmp_device_count(int* n);
 int tcmp_version(void);
 /* profiling builds (-DTCMP_PROF) only: k_edges clock breakdown accumulated since create
  * (total, work fetch, collision, torque, bookkeeping, tier-4 exact, ...) and exact-test
- * outcome counts (12..19), n <= 20; zeros otherwise. */
+ * outcome counts (12..27), n <= 28; zeros otherwise. */
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n);
 
 /* Fixed obstacles (replaces Problem.fixed bodies + pybullet getClosestPoints,
@@ -66,6 +66,24 @@ int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs);
 int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off,
                     const double* planes, const int32_t* plane_off, const int32_t* edges,
                     const int32_t* edge_off, const double* boxes, int32_t n_mesh);
+
+/* A set of n hulls in tcmp_set_meshes' layout (world frame, rows [off[m], off[m+1])). */
+typedef struct tcmp_hulls {
+  const double* verts;        /* V x 3 */
+  const int32_t* vert_off;    /* n + 1 */
+  const double* planes;       /* F x 4: unit outward n, d */
+  const int32_t* plane_off;
+  const int32_t* edges;       /* E x 4: va vb f1 f2 (hull-local rows) */
+  const int32_t* edge_off;
+} tcmp_hulls;
+
+/* Optional level-of-detail hulls for the current meshes (same count, call after
+ * tcmp_set_meshes): inner[m] must lie inside mesh m's hull and outer[m] must contain it.
+ * The kernels use them only as certificates before the exact test ("free" when the outer
+ * hulls' depth is below 0.04 - 1e-4, "collision" when the inner hulls' depth exceeds
+ * 0.04 + 1e-4), so results do not depend on them -- only speed.  hull.py builds them. */
+int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls* outer,
+                       int32_t n_mesh);
 
 /* ---- batched physics (host arrays in/out) ---------------------------------------------- */
 /* rne(q, qd, qdd) with add_payload(r, m) state made explicit: payload iff payload_mass > 0

@@ -19,12 +19,40 @@ def test_cube_hull_merges_coplanar_facets():
             assert np.allclose(v[[a, b]] @ pl[f, :3], pl[f, 3])
 
 
+def sat_pd(A, B):
+    """Brute-force penetration depth of hulls A, B ((verts, planes, edges)): the minimum
+    over every candidate axis of the Minkowski difference's support (A facets, -B facets,
+    both signs of every edge-pair cross product)."""
+    Av, Bv = A[0], B[0]
+    ea = Av[A[2][:, 1]] - Av[A[2][:, 0]]
+    eb = Bv[B[2][:, 1]] - Bv[B[2][:, 0]]
+    c = np.cross(ea[:, None, :], eb[None, :, :]).reshape(-1, 3)
+    n = np.linalg.norm(c, axis=1)
+    c = c[n > 1e-12] / n[n > 1e-12, None]
+    U = np.vstack([A[1][:, :3], -B[1][:, :3], c, -c])
+    return ((Av @ U.T).max(0) - (Bv @ U.T).min(0)).min()
+
+
 def test_boxes_contain_and_are_contained():
     rng = np.random.default_rng(0)
     for name, verts in hull.library_shapes().items():
         m = scene.ConvexMesh(verts, rotation=scene.random_rotation(rng),
                              position=rng.uniform(-1, 1, 3), scale=rng.uniform(0.5, 1.5))
-        v, pl, e, box = m.record()
+        v, pl, e, box, inner, outer = m.record()
+        # level-of-detail hulls: inner inside the hull, hull inside outer
+        assert (inner[0] @ pl[:, :3].T <= pl[:, 3] + 1e-12).all(), name
+        assert (v @ outer[1][:, :3].T <= outer[1][:, 3] + 1e-12).all(), name
+        assert len(inner[0]) <= 24 and len(inner[2]) < len(e) or len(v) <= 24
+        for h in (inner, outer):  # no zero-length edges (the kernels take edge vectors from
+            ev = h[0][h[2][:, 1]] - h[0][h[2][:, 0]]  # fp64 differences, so short ones are fine)
+            assert np.linalg.norm(ev, axis=1).min() > 1e-9, name
+        # penetration depth is monotone under inclusion: inner <= exact <= outer
+        for _ in range(3):
+            R, t = scene.random_rotation(rng), rng.uniform(-1, 1, 3) * 0.05 + v.mean(0)
+            lk = (v - v.mean(0)) @ R.T * 0.3 + t  # a smaller hull near the middle
+            L = hull.hull_data(lk)
+            d = [sat_pd(L, h) for h in (inner, (v, pl, e), outer)]
+            assert d[0] <= d[1] + 1e-12 and d[1] <= d[2] + 1e-12, (name, d)
         c, R, h, ih = box[:3], box[3:12].reshape(3, 3), box[12:15], box[15:18]
         assert np.allclose(R.T @ R, np.eye(3), atol=1e-12)
         loc = (v - c) @ R

@@ -20,7 +20,7 @@ def main():
     eng = _lib.Engine(0)
     obs, pack, goal = bench.make_query(1234, n_obs=0, n_mesh=W["meshes"], engine=eng)
     r, _ = bench.run_query(eng, obs, goal, n, W["batch"], 1234, meshes=pack)
-    c = eng.debug_counters(20)
+    c = eng.debug_counters(28)
     tot = max(1, c[0])
     print(json.dumps({"samples": n, "ms_edges": r.ms_edges, "ms_nearest": r.ms_nearest,
                       "edge_steps": r.edge_steps, "pairs_tested": r.pairs_tested,
@@ -29,8 +29,11 @@ def main():
                                     "torque": c[3] / tot, "tail": c[4] / tot,
                                     "exact_in_collision": c[5] / tot, "sincos": c[6] / tot,
                                     "tiers123_in_collision": c[7] / tot},
-                      "mesh_exact": {"outer_box_free": c[16], "inner_box_collision": c[17],
-                                     "hull_hull_fp32": c[18], "hull_hull_fp64": c[19]}}),
+                      "mesh_exact": {"outer_box_free": c[16], "outer_lod_free": c[17],
+                                     "inner_collision": c[18], "hull_hull_fp64": c[19]},
+                      "hull_hull_exits": {"mesh_facets": c[20], "link_facets": c[21],
+                                          "edges_early": c[22], "full_collision": c[23],
+                                          "full_free": c[24], "degenerate": c[25]}}),
           flush=True)
 
 

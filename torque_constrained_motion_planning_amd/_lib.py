@@ -23,7 +23,7 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 # C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
-    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk", "tcmp_debug_counters",
@@ -40,6 +40,12 @@ class PlanCfg(ctypes.Structure):
         ("max_nodes", ctypes.c_int64), ("max_batch", ctypes.c_int32),
         ("torque_mode", ctypes.c_int32),
     ]
+
+
+class Hulls(ctypes.Structure):
+    """struct tcmp_hulls"""
+    _fields_ = [("verts", _dp), ("vert_off", _i32p), ("planes", _dp), ("plane_off", _i32p),
+                ("edges", _i32p), ("edge_off", _i32p)]
 
 
 class PlanResult(ctypes.Structure):
@@ -86,6 +92,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
         L.tcmp_set_scene.argtypes = [vp, _dp, ctypes.c_int32]
         L.tcmp_set_meshes.argtypes = [vp, _dp, _i32p, _dp, _i32p, _i32p, _i32p, _dp, ctypes.c_int32]
+        L.tcmp_set_mesh_lods.argtypes = [vp, ctypes.POINTER(Hulls), ctypes.POINTER(Hulls),
+                                         ctypes.c_int32]
         L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
                                      ctypes.c_double, _i32p]
@@ -183,6 +191,18 @@ class Engine:
             self._check(self.L.tcmp_set_meshes(self.h, _d(arrs[0]), ip(arrs[1]), _d(arrs[2]),
                                                ip(arrs[3]), ip(arrs[4]), ip(arrs[5]),
                                                _d(arrs[6]), int(len(meshes))))
+            if getattr(meshes, "inner", None) is not None:
+                keep = []
+
+                def hulls(hs):
+                    a = (np.ascontiguousarray(hs.verts, dtype=np.float64), i32(hs.vert_off),
+                         np.ascontiguousarray(hs.planes, dtype=np.float64), i32(hs.plane_off),
+                         i32(hs.edges), i32(hs.edge_off))
+                    keep.append(a)
+                    return Hulls(_d(a[0]), ip(a[1]), _d(a[2]), ip(a[3]), ip(a[4]), ip(a[5]))
+                hi, ho = hulls(meshes.inner), hulls(meshes.outer)
+                self._check(self.L.tcmp_set_mesh_lods(self.h, ctypes.byref(hi), ctypes.byref(ho),
+                                                      int(len(meshes))))
         self._mesh_key = mkey
         self._scene_key = key
 

@@ -18,6 +18,7 @@
 
 #define TCMP_GEO_QUAL static constexpr
 #include "panda_geometry.inc"
+#include "panda_lod.inc"
 
 namespace tcmp {
 
@@ -94,7 +95,8 @@ struct Scene {
   const float* __restrict__ obs32;   // [n][8]: world-AABB centre(3), H - kPen + margin (3)
   unsigned* wq;                      // this wave's LDS pair queue (collides_wave), kQcap + 2
   // convex-mesh obstacles (tcmp_set_meshes), world frame, global memory
-  const int* __restrict__ mrange;    // [m][8]: v0 v1 f0 f1 e0 e1 (rows of the arrays below)
+  const int* __restrict__ mrange;    // [m][24]: v0 v1 f0 f1 e0 e1 (rows of the arrays below),
+                                     // the same for the inner / outer LODs, has-LOD flag
   const double* __restrict__ mib;    // [m][16]: inner box record (c, B, inner half, 0)
   const double4* __restrict__ mv64;  // [V]: x y z 0
   const float4* __restrict__ mv32;
@@ -102,7 +104,20 @@ struct Scene {
   const float4* __restrict__ mp32;
   const double* __restrict__ me64;   // [E][16]: c = -n1, d = -n2, dxc = unit(d x c), e, v0
   const float* __restrict__ me32;    // [E][16]
+  // level-of-detail hulls of the meshes ([0] inner, [1] outer; mrange [6..17], flag [18])
+  const float4* lv32[2];
+  const float4* lp32[2];
+  const float* le32[2];
+  // the links' level-of-detail hulls (panda_lod.inc), fp32 link frames: [0] inner, [1] outer
+  const float* lodv3[2];
+  const float4* lodpl[2];
+  const ushort4* lodei[2];
+  // edge vectors vb - va of the link hulls (fp64 differences rounded to fp32: an fp32
+  // difference of nearby vertices would lose the direction of short edges)
+  const float4* lodev[2];
+  const float4* geo_ev;
 };
+constexpr int kMrange = 24;  // ints per mesh in Scene::mrange
 __device__ __forceinline__ int obs_mesh(const double* ob) {
   return ob[15] < 0.0 ? (int)(-ob[15]) - 1 : -1;
 }
@@ -121,9 +136,27 @@ __host__ __device__ constexpr unsigned scene_lds_bytes(int n_obs) {
 __host__ __device__ constexpr unsigned stage_lds_bytes(int n_obs) {
   return scene_lds_bytes(n_obs) + geo_lds_bytes() + 4 * kQwaveBytes;  // 256-thread blocks
 }
+// Mesh scenes (up to kMaxObstacles records, hull-vs-hull exact tests) stage only the fp32
+// tier-0 records and the pair queues, so that LDS does not cap residency at one 256-thread
+// block per CU; the fp64 records and the hull geometry are then read through the caches.
+__host__ __device__ constexpr unsigned stage_lds_bytes_lean(int n_obs) {
+  return (unsigned)(n_obs > 0 ? n_obs : 1) * (8 * sizeof(float)) + 4 * kQwaveBytes;
+}
+template <bool FULL>
 __device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* lds, Scene& so,
                                           Geo& go) {
   const int n = sc.n_obs > 0 ? sc.n_obs : 1;
+  if (!FULL) {
+    float* o32 = reinterpret_cast<float*>(lds);
+    unsigned* wq = reinterpret_cast<unsigned*>(o32 + 8 * n) + (threadIdx.x >> 6) * (kQwaveBytes / 4);
+    for (int i = threadIdx.x; i < sc.n_obs * 8; i += blockDim.x) o32[i] = sc.obs32[i];
+    __syncthreads();
+    so = sc;
+    so.obs32 = o32;
+    so.wq = wq;
+    go = g;
+    return;
+  }
   double* o64 = lds;
   float* o32 = reinterpret_cast<float*>(lds + 16 * n);
   float4* pl = reinterpret_cast<float4*>(o32 + 8 * n);
@@ -535,7 +568,8 @@ constexpr float kExactGuard = 1e-4f;
 #ifdef TCMP_PROF_EXACT
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
-__device__ unsigned long long g_exact_stats[8];  // [4..7]: mesh pairs (exact_pair)
+__device__ unsigned long long g_exact_stats[16];  // [4..7]: mesh pairs (exact_pair),
+                                                  // [8..13]: exact_mesh_wave32 exits
 #endif
 __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g) {
@@ -681,15 +715,45 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
 #else
 #define TCMP_MESH_STAT(i)
 #endif
+  constexpr float P = (float)kPen;
+  const int* rg = sc.mrange + kMrange * mi;
   const float po = exact_pd_wave32(link, PL, ob, g);
-  if (po == po && po < (float)kPen - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
-  const double* ib = sc.mib + 16 * mi;
-  if (ib[12] > 0.0) {
-    const float pi = exact_pd_wave32(link, PL, ib, g);
-    if (pi == pi && pi > (float)kPen + kExactGuard) { TCMP_MESH_STAT(5); return (double)pi; }
+  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
+  float R[9], p[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = (float)PL.R[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = (float)PL.p[k];
+  if (rg[18]) {
+    // level-of-detail certificates: outer LODs contain the hulls ("free" below kPen - guard),
+    // inner LODs lie inside them ("collision" above kPen + guard)
+    const HullA32 Ao{sc.lodv3[1], sc.lodpl[1], sc.lodei[1], sc.lodev[1], tcmp_lod_out_vert_off[link],
+                     tcmp_lod_out_vert_off[link + 1], tcmp_lod_out_plane_off[link],
+                     tcmp_lod_out_plane_off[link + 1], tcmp_lod_out_edge_off[link],
+                     tcmp_lod_out_edge_off[link + 1]};
+    const HullB32 Bo{sc.lv32[1], sc.lp32[1], sc.le32[1], rg[12], rg[13], rg[14], rg[15], rg[16], rg[17]};
+    const float pl = hull_hull_wave32<false>(Ao, Bo, R, p, P - kExactGuard);
+    if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); return (double)pl; }
+    const HullA32 Ai{sc.lodv3[0], sc.lodpl[0], sc.lodei[0], sc.lodev[0], tcmp_lod_in_vert_off[link],
+                     tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
+                     tcmp_lod_in_plane_off[link + 1], tcmp_lod_in_edge_off[link],
+                     tcmp_lod_in_edge_off[link + 1]};
+    const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11]};
+    const float pi = hull_hull_wave32<false>(Ai, Bi, R, p, P + kExactGuard);
+    if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+  } else {
+    const double* ib = sc.mib + 16 * mi;
+    if (ib[12] > 0.0) {
+      const float pi = exact_pd_wave32(link, PL, ib, g);
+      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+    }
   }
-  const float pm = exact_mesh_wave32(link, PL, mi, sc, g);
-  if (pm == pm && fabsf(pm - (float)kPen) > kExactGuard) { TCMP_MESH_STAT(6); return (double)pm; }
+  const HullA32 A{g.verts32, g.planes32, g.eidx, sc.geo_ev, tcmp_geo_vert_off[link],
+                  tcmp_geo_vert_off[link + 1], tcmp_geo_plane_off[link],
+                  tcmp_geo_plane_off[link + 1], tcmp_geo_edge_off[link], tcmp_geo_edge_off[link + 1]};
+  const HullB32 B{sc.mv32, sc.mp32, sc.me32, rg[0], rg[1], rg[2], rg[3], rg[4], rg[5]};
+  const float pm = hull_hull_wave32<true>(A, B, R, p, P - kExactGuard);
+  if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;
   TCMP_MESH_STAT(7);
   return exact_mesh_wave(link, PL, mi, sc, g);
 #undef TCMP_MESH_STAT

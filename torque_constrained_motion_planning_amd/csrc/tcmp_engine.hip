@@ -336,7 +336,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
-  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
+  stage_lds<!MESH>(sc_g, g_g, tcmp_lds, sc, g);
   const int lane = lane_id();
   int e = -1, i = 0, n = 0;
   bool done = false;
@@ -499,7 +499,7 @@ __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
-  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
+  stage_lds<!MESH>(sc_g, g_g, tcmp_lds, sc, g);
   const long long R = st->rw_count, T = st->snap;
   const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = t < R && ncount[t] > 0;
@@ -764,7 +764,7 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
-  stage_lds(sc_g, g_g, tcmp_lds, sc, g);
+  stage_lds<!MESH>(sc_g, g_g, tcmp_lds, sc, g);
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool act = i < n;
   double x[7];
@@ -882,8 +882,13 @@ struct tcmp_handle {
   std::vector<double> mesh_v, mesh_p, mesh_box;
   std::vector<int> mesh_e, mesh_voff, mesh_poff, mesh_eoff;
   DBuf<int> mrange;
+  std::vector<int> mrange_h;
   DBuf<double> mib, mv64, mp64, me64;
   DBuf<float> mv32, mp32, me32;
+  DBuf<float> lv32[2], lp32[2], le32[2];      // mesh LOD hulls (inner, outer), world frame
+  DBuf<float> lodv3[2], lodpl[2];             // link LOD hulls (panda_lod.inc), link frames
+  DBuf<unsigned short> lodei[2];
+  DBuf<float> lodev[2], geo_ev;               // link hull edge vectors (fp64 -> fp32)
   DevState* st = nullptr;
   // plan
   PlanParams P{};
@@ -941,6 +946,16 @@ struct tcmp_handle {
     s.mp32 = reinterpret_cast<const float4*>(mp32.p);
     s.me64 = me64.p;
     s.me32 = me32.p;
+    for (int i = 0; i < 2; ++i) {
+      s.lv32[i] = reinterpret_cast<const float4*>(lv32[i].p);
+      s.lp32[i] = reinterpret_cast<const float4*>(lp32[i].p);
+      s.le32[i] = le32[i].p;
+      s.lodv3[i] = lodv3[i].p;
+      s.lodpl[i] = reinterpret_cast<const float4*>(lodpl[i].p);
+      s.lodei[i] = reinterpret_cast<const ushort4*>(lodei[i].p);
+      s.lodev[i] = reinterpret_cast<const float4*>(lodev[i].p);
+    }
+    s.geo_ev = reinterpret_cast<const float4*>(geo_ev.p);
     return s;
   }
 
@@ -994,6 +1009,10 @@ int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
+}
+
+unsigned lds_bytes(const tcmp_handle* h) {
+  return h->n_mesh ? stage_lds_bytes_lean(h->n_obs) : stage_lds_bytes(h->n_obs);
 }
 
 unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>(1, (n + block - 1) / block); }
@@ -1111,7 +1130,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(h->n_mesh ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), stage_lds_bytes(h->n_obs), h->stream, J, P,
+  hipLaunchKernelGGL(h->n_mesh ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, P,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1143,15 +1162,15 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (int rc = set_dev(h)) return rc;
-  if (!out || n < 0 || n > 20) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 28) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   for (int i = 0; i < n; ++i) out[i] = s.prof[i];
 #ifdef TCMP_PROF_EXACT
-  unsigned long long ex[8];
+  unsigned long long ex[16];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
-  for (int i = 0; i < 8 && 12 + i < n; ++i) out[12 + i] = ex[i];
+  for (int i = 0; i < 16 && 12 + i < n; ++i) out[12 + i] = ex[i];
 #endif
   return 0;
 }
@@ -1196,6 +1215,40 @@ int tcmp_create(int device, tcmp_handle** out) {
     HIPCHK(hipMemcpy(h->verts32.p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->planes32.p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(h->eidx.p, tcmp_geo_edge_idx, sizeof(tcmp_geo_edge_idx), hipMemcpyHostToDevice));
+    {
+      std::vector<float> ev(4 * TCMP_TOTAL_EDGES, 0.f);
+      for (int e = 0; e < TCMP_TOTAL_EDGES; ++e) {
+        const unsigned short* q = tcmp_geo_edge_idx + 4 * e;
+        for (int k = 0; k < 3; ++k)
+          ev[4 * e + k] = (float)(tcmp_geo_verts[4 * q[1] + k] - tcmp_geo_verts[4 * q[0] + k]);
+      }
+      rc = h->geo_ev.ensure(ev.size());
+      if (rc) { delete h; return rc; }
+      HIPCHK(hipMemcpy(h->geo_ev.p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
+    }
+    // link LOD hulls (fp32 vertices [V][3], planes float4, edge rows)
+    const double* lv[2] = {tcmp_lod_in_verts, tcmp_lod_out_verts};
+    const double* lp[2] = {tcmp_lod_in_planes, tcmp_lod_out_planes};
+    const unsigned short* le[2] = {tcmp_lod_in_edges, tcmp_lod_out_edges};
+    const size_t nv[2] = {TCMP_LOD_IN_V, TCMP_LOD_OUT_V}, nf[2] = {TCMP_LOD_IN_F, TCMP_LOD_OUT_F},
+                 ne[2] = {TCMP_LOD_IN_E, TCMP_LOD_OUT_E};
+    for (int i = 0; i < 2; ++i) {
+      std::vector<float> a(lv[i], lv[i] + 3 * nv[i]), b(lp[i], lp[i] + 4 * nf[i]);
+      rc = h->lodv3[i].ensure(a.size());
+      rc = rc ? rc : h->lodpl[i].ensure(b.size());
+      rc = rc ? rc : h->lodei[i].ensure(4 * ne[i]);
+      if (rc) { delete h; return rc; }
+      HIPCHK(hipMemcpy(h->lodv3[i].p, a.data(), a.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(h->lodpl[i].p, b.data(), b.size() * 4, hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(h->lodei[i].p, le[i], 4 * ne[i] * sizeof(unsigned short), hipMemcpyHostToDevice));
+      std::vector<float> ev(4 * ne[i], 0.f);
+      for (size_t e = 0; e < ne[i]; ++e)
+        for (int k = 0; k < 3; ++k)
+          ev[4 * e + k] = (float)(lv[i][3 * le[i][4 * e + 1] + k] - lv[i][3 * le[i][4 * e] + k]);
+      rc = h->lodev[i].ensure(ev.size());
+      if (rc) { delete h; return rc; }
+      HIPCHK(hipMemcpy(h->lodev[i].p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
+    }
     // dynamic LDS above 64 KiB per workgroup must be allowed explicitly
     const int lim = (int)stage_lds_bytes(kMaxObstacles);
     for (const void* k : {(const void*)k_edges<false>, (const void*)k_edges<true>,
@@ -1219,10 +1272,16 @@ int tcmp_destroy(tcmp_handle* h) {
   h->verts32.release();
   h->planes32.release();
   h->eidx.release();
+  h->geo_ev.release();
   h->obs32.release();
   h->mrange.release();
   for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64}) b->release();
   for (auto* b : {&h->mv32, &h->mp32, &h->me32}) b->release();
+  for (int i = 0; i < 2; ++i) {
+    for (auto* b : {&h->lv32[i], &h->lp32[i], &h->le32[i], &h->lodv3[i], &h->lodpl[i], &h->lodev[i]})
+      b->release();
+    h->lodei[i].release();
+  }
   for (auto* b : {&h->verts, &h->planes, &h->edges, &h->obs, &h->cfg, &h->tgt, &h->cand,
                   &h->last, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
                   &h->s1, &h->s2, &h->s3})
@@ -1272,6 +1331,47 @@ namespace {
 
 // Device obstacle list = boxes then the meshes' outer boxes (records of 16 doubles, kind in
 // [15]) plus the fp32 tier-0 records (world AABB centre, half extent - kPen + margin).
+// Gauss-map edge records of world-frame hulls (rows of 16): c = -n1, d = -n2 (the obstacle
+// enters the Minkowski difference negated), unit(d x c), edge vector vb - va, endpoint va.
+void edge_records(const double* verts, const int32_t* vert_off, const double* planes,
+                  const int32_t* plane_off, const int32_t* edges, const int32_t* edge_off,
+                  int n, double* out) {
+  for (int m = 0; m < n; ++m)
+    for (int e = edge_off[m]; e < edge_off[m + 1]; ++e) {
+      const int* q = edges + 4 * e;
+      const double* va = verts + 3 * (vert_off[m] + q[0]);
+      const double* vb = verts + 3 * (vert_off[m] + q[1]);
+      const double* n1 = planes + 4 * (plane_off[m] + q[2]);
+      const double* n2 = planes + 4 * (plane_off[m] + q[3]);
+      double* o = out + 16 * e;
+      for (int k = 0; k < 3; ++k) { o[k] = -n1[k]; o[3 + k] = -n2[k]; }
+      double w[3] = {o[4] * o[2] - o[5] * o[1], o[5] * o[0] - o[3] * o[2], o[3] * o[1] - o[4] * o[0]};
+      const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
+      for (int k = 0; k < 3; ++k) o[6 + k] = wl > 0 ? w[k] / wl : 0.0;
+      for (int k = 0; k < 3; ++k) { o[9 + k] = vb[k] - va[k]; o[12 + k] = va[k]; }
+      o[15] = 0.0;
+    }
+}
+
+int check_hulls(const tcmp_hulls* H, int n, const char* what) {
+  if (!H || !H->verts || !H->vert_off || !H->planes || !H->plane_off || !H->edges || !H->edge_off)
+    return fail(-1, std::string("null ") + what + " hull array");
+  if (H->vert_off[0] != 0 || H->plane_off[0] != 0 || H->edge_off[0] != 0)
+    return fail(-1, std::string(what) + " hull offsets must start at 0");
+  for (int m = 0; m < n; ++m) {
+    const int nv = H->vert_off[m + 1] - H->vert_off[m], nf = H->plane_off[m + 1] - H->plane_off[m];
+    if (nv < 4 || nf < 4 || H->edge_off[m + 1] - H->edge_off[m] < 6)
+      return fail(-1, std::string(what) + " hull " + std::to_string(m) + " is not a 3-D hull");
+    for (int e = H->edge_off[m]; e < H->edge_off[m + 1]; ++e) {
+      const int* q = H->edges + 4 * e;
+      if (q[0] < 0 || q[0] >= nv || q[1] < 0 || q[1] >= nv || q[2] < 0 || q[2] >= nf || q[3] < 0 ||
+          q[3] >= nf)
+        return fail(-1, std::string(what) + " hull " + std::to_string(m) + ": edge index out of range");
+    }
+  }
+  return 0;
+}
+
 int upload_scene(tcmp_handle* h) {
   const int n = h->n_box + h->n_mesh;
   std::vector<double> tmp((size_t)std::max(n, 1) * 16, 0.0);
@@ -1383,12 +1483,12 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
     h->mesh_eoff.assign(1, 0);
   }
   // device records: vertex/plane rows, Gauss-map edge records (global rows), inner boxes
-  std::vector<int> rg((size_t)std::max(n_mesh, 1) * 8, 0);
+  std::vector<int> rg((size_t)std::max(n_mesh, 1) * kMrange, 0);
   std::vector<double> ib((size_t)std::max(n_mesh, 1) * 16, 0.0);
   std::vector<double> v64((size_t)std::max(V, 1) * 4, 0.0), p64((size_t)std::max(F, 1) * 4, 0.0),
       e64((size_t)std::max(E, 1) * 16, 0.0);
   for (int m = 0; m < n_mesh; ++m) {
-    int* r = rg.data() + 8 * m;
+    int* r = rg.data() + kMrange * m;
     r[0] = vert_off[m]; r[1] = vert_off[m + 1];
     r[2] = plane_off[m]; r[3] = plane_off[m + 1];
     r[4] = edge_off[m]; r[5] = edge_off[m + 1];
@@ -1396,21 +1496,8 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
     double* d = ib.data() + 16 * m;
     for (int k = 0; k < 12; ++k) d[k] = b[k];
     for (int k = 0; k < 3; ++k) d[12 + k] = b[15 + k];
-    for (int e = edge_off[m]; e < edge_off[m + 1]; ++e) {
-      const int* q = edges + 4 * e;
-      const double* va = verts + 3 * (vert_off[m] + q[0]);
-      const double* vb = verts + 3 * (vert_off[m] + q[1]);
-      const double* n1 = planes + 4 * (plane_off[m] + q[2]);
-      const double* n2 = planes + 4 * (plane_off[m] + q[3]);
-      double* o = e64.data() + 16 * e;
-      // c = -n1, d = -n2 (the obstacle enters the Minkowski difference negated), d x c
-      for (int k = 0; k < 3; ++k) { o[k] = -n1[k]; o[3 + k] = -n2[k]; }
-      double w[3] = {o[4] * o[2] - o[5] * o[1], o[5] * o[0] - o[3] * o[2], o[3] * o[1] - o[4] * o[0]};
-      const double wl = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
-      for (int k = 0; k < 3; ++k) o[6 + k] = wl > 0 ? w[k] / wl : 0.0;
-      for (int k = 0; k < 3; ++k) { o[9 + k] = vb[k] - va[k]; o[12 + k] = va[k]; }
-    }
   }
+  edge_records(verts, vert_off, planes, plane_off, edges, edge_off, n_mesh, e64.data());
   for (int v = 0; v < V; ++v)
     for (int k = 0; k < 3; ++k) v64[4 * v + k] = verts[3 * v + k];
   for (int f = 0; f < F; ++f)
@@ -1426,6 +1513,7 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
   rc = rc ? rc : h->me32.ensure(e32.size());
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  h->mrange_h = rg;
   HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mp64.p, p64.data(), p64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -1436,6 +1524,45 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
   HIPCHK(hipStreamSynchronize(h->stream));
   h->n_mesh = n_mesh;
   return upload_scene(h);
+}
+
+int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls* outer,
+                       int32_t n_mesh) {
+  if (int rc = set_dev(h)) return rc;
+  if (n_mesh != h->n_mesh) return fail(-1, "LOD count differs from the mesh count");
+  if (n_mesh == 0) return 0;
+  if (int rc = check_hulls(inner, n_mesh, "inner")) return rc;
+  if (int rc = check_hulls(outer, n_mesh, "outer")) return rc;
+  const tcmp_hulls* H[2] = {inner, outer};
+  std::vector<int> rg = h->mrange_h;
+  for (int i = 0; i < 2; ++i) {
+    const int V = H[i]->vert_off[n_mesh], F = H[i]->plane_off[n_mesh], E = H[i]->edge_off[n_mesh];
+    std::vector<double> e64((size_t)E * 16);
+    edge_records(H[i]->verts, H[i]->vert_off, H[i]->planes, H[i]->plane_off, H[i]->edges,
+                 H[i]->edge_off, n_mesh, e64.data());
+    std::vector<float> v32((size_t)V * 4, 0.f), p32(H[i]->planes, H[i]->planes + 4 * (size_t)F),
+        e32(e64.begin(), e64.end());
+    for (int v = 0; v < V; ++v)
+      for (int k = 0; k < 3; ++k) v32[4 * v + k] = (float)H[i]->verts[3 * v + k];
+    int rc = h->lv32[i].ensure(v32.size());
+    rc = rc ? rc : h->lp32[i].ensure(p32.size());
+    rc = rc ? rc : h->le32[i].ensure(e32.size());
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h->lv32[i].p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->lp32[i].p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->le32[i].p, e32.data(), e32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    for (int m = 0; m < n_mesh; ++m) {
+      int* r = rg.data() + kMrange * m + 6 + 6 * i;
+      r[0] = H[i]->vert_off[m]; r[1] = H[i]->vert_off[m + 1];
+      r[2] = H[i]->plane_off[m]; r[3] = H[i]->plane_off[m + 1];
+      r[4] = H[i]->edge_off[m]; r[5] = H[i]->edge_off[m + 1];
+    }
+  }
+  for (int m = 0; m < n_mesh; ++m) rg[kMrange * m + 18] = 1;
+  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->mrange_h = rg;
+  return 0;
 }
 
 int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
@@ -1528,7 +1655,7 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   int rc = upload7(h, h->s0, q, n);
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
-  hipLaunchKernelGGL(h->n_mesh ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, h->s0.p,
+  hipLaunchKernelGGL(h->n_mesh ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
                      (long long)n, h->scene(), h->geo(), h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
@@ -1822,7 +1949,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(h->n_mesh ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), stage_lds_bytes(h->n_obs), h->stream, P, h->st,
+  hipLaunchKernelGGL(h->n_mesh ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), lds_bytes(h), h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);

@@ -23,37 +23,54 @@
 
 namespace tcmp {
 
-__device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, int m,
-                                                   const Scene sc, const Geo g) {
+#ifdef TCMP_PROF_EXACT
+#define TCMP_MSTAT(i) if (lane_id() == 0) atomicAdd(&g_exact_stats[i], 1ull)
+#else
+#define TCMP_MSTAT(i)
+#endif
+
+// A hull in a link frame (rotated per lane into the world): vertices [V][3], planes (n, d),
+// edges (va, vb, f1, f2) as rows of those arrays; [x0, x1) ranges of this hull.
+struct HullA32 {
+  const float* v3;
+  const float4* pl;
+  const ushort4* ei;
+  const float4* ev;  // [E]: vb - va (rounded from fp64)
+  int v0, v1, f0, f1, e0, e1;
+};
+// A world-frame obstacle hull: vertices, planes, Gauss-map edge records [E][16]
+// (c = -n1, d = -n2, unit(d x c), edge vector, endpoint).
+struct HullB32 {
+  const float4* v;
+  const float4* pl;
+  const float* er;
+  int v0, v1, f0, f1, e0, e1;
+};
+
+// fp32 penetration depth of hull A (pose R, p) against hull B, wave-cooperative.  Returns as
+// soon as a stage's minimum falls below `stop` (then the value is only an upper bound below
+// `stop`), NaN when an edge axis is too degenerate for fp32 (see the header comment).
+template <bool STAT>
+__device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32 B,
+                                                  const float R[9], const float p[3], float stop) {
   const int lane = lane_id();
-  const int* rg = sc.mrange + 8 * m;
-  const int v0 = rg[0], v1 = rg[1], f0 = rg[2], f1 = rg[3], e0 = rg[4], e1 = rg[5];
-  const int lv0 = tcmp_geo_vert_off[link], lv1 = tcmp_geo_vert_off[link + 1];
-  const int lf0 = tcmp_geo_plane_off[link], lf1 = tcmp_geo_plane_off[link + 1];
-  const int le0 = tcmp_geo_edge_off[link], le1 = tcmp_geo_edge_off[link + 1];
-  float R[9], p[3];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = (float)pose.R[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = (float)pose.p[k];
-  constexpr float P = (float)kPen;
   float loc = INFINITY;
-  // (1) mesh facets (moved into the link frame) against the link's vertices (LDS broadcast)
-  for (int base = f0; base < f1; base += 256) {
+  // (1) B's facets (moved into A's frame) against A's vertices (uniform stream)
+  for (int base = B.f0; base < B.f1; base += 256) {
     float nx[4], ny[4], nz[4], dd[4], mn[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int f = base + lane + 64 * j;
       float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
-      if (f < f1) w = sc.mp32[f];
+      if (f < B.f1) w = B.pl[f];
       nx[j] = R[0] * w.x + R[3] * w.y + R[6] * w.z;
       ny[j] = R[1] * w.x + R[4] * w.y + R[7] * w.z;
       nz[j] = R[2] * w.x + R[5] * w.y + R[8] * w.z;
       dd[j] = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
       mn[j] = INFINITY;
     }
-    for (int v = lv0; v < lv1; ++v) {
-      const float x = g.verts32[3 * v], y = g.verts32[3 * v + 1], z = g.verts32[3 * v + 2];
+    for (int v = A.v0; v < A.v1; ++v) {
+      const float x = A.v3[3 * v], y = A.v3[3 * v + 1], z = A.v3[3 * v + 2];
 #pragma unroll
       for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
     }
@@ -61,23 +78,23 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
     for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
   }
   float pd = wave_minf(loc);
-  if (pd < P - kExactGuard) return pd;
-  // (2) link facets (moved into the world frame) against the mesh's vertices
-  for (int base = lf0; base < lf1; base += 256) {
+  if (pd < stop) { if (STAT) TCMP_MSTAT(8); return pd; }
+  // (2) A's facets (moved into the world frame) against B's vertices
+  for (int base = A.f0; base < A.f1; base += 256) {
     float nx[4], ny[4], nz[4], dd[4], mn[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int f = base + lane + 64 * j;
       float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
-      if (f < lf1) w = g.planes32[f];
+      if (f < A.f1) w = A.pl[f];
       nx[j] = R[0] * w.x + R[1] * w.y + R[2] * w.z;
       ny[j] = R[3] * w.x + R[4] * w.y + R[5] * w.z;
       nz[j] = R[6] * w.x + R[7] * w.y + R[8] * w.z;
       dd[j] = w.w + (nx[j] * p[0] + ny[j] * p[1] + nz[j] * p[2]);
       mn[j] = INFINITY;
     }
-    for (int v = v0; v < v1; ++v) {
-      const float4 P4 = sc.mv32[v];
+    for (int v = B.v0; v < B.v1; ++v) {
+      const float4 P4 = B.v[v];
 #pragma unroll
       for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * P4.x + ny[j] * P4.y + nz[j] * P4.z);
     }
@@ -85,18 +102,18 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
     for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
   }
   pd = fminf(pd, wave_minf(loc));
-  if (pd < P - kExactGuard) return pd;
-  // (3) edge pairs: lanes own link edges, the mesh's edges stream wave-uniformly
+  if (pd < stop) { if (STAT) TCMP_MSTAT(9); return pd; }
+  // (3) edge pairs: lanes own A's edges, B's edges stream wave-uniformly
   bool deg = false;
-  for (int base = le0; base < le1; base += 64) {
+  for (int base = A.e0; base < A.e1; base += 64) {
     const int e = base + lane;
-    const bool valid = e < le1;
+    const bool valid = e < A.e1;
     float ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;  // adjacent facet normals (world)
     float ux = 0, uy = 0, uz = 0;                          // unit(b x a)
     float ex = 0, ey = 0, ez = 0, px = 0, py = 0, pz = 0;  // edge vector, endpoint (world)
     if (valid) {
-      const ushort4 ix = g.eidx[e];
-      const float4 na = g.planes32[ix.z], nb = g.planes32[ix.w];
+      const ushort4 ix = A.ei[e];
+      const float4 na = A.pl[ix.z], nb = A.pl[ix.w];
       ax = R[0] * na.x + R[1] * na.y + R[2] * na.z;
       ay = R[3] * na.x + R[4] * na.y + R[5] * na.z;
       az = R[6] * na.x + R[7] * na.y + R[8] * na.z;
@@ -108,9 +125,9 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
       uz = bx * ay - by * ax;
       const float il = rsqrtf(ux * ux + uy * uy + uz * uz);
       ux *= il; uy *= il; uz *= il;
-      const float x0 = g.verts32[3 * ix.x], y0 = g.verts32[3 * ix.x + 1], z0 = g.verts32[3 * ix.x + 2];
-      const float lx = g.verts32[3 * ix.y] - x0, ly = g.verts32[3 * ix.y + 1] - y0,
-                  lz = g.verts32[3 * ix.y + 2] - z0;
+      const float x0 = A.v3[3 * ix.x], y0 = A.v3[3 * ix.x + 1], z0 = A.v3[3 * ix.x + 2];
+      const float4 ed = A.ev[e];
+      const float lx = ed.x, ly = ed.y, lz = ed.z;
       ex = R[0] * lx + R[1] * ly + R[2] * lz;
       ey = R[3] * lx + R[4] * ly + R[5] * lz;
       ez = R[6] * lx + R[7] * ly + R[8] * lz;
@@ -119,8 +136,9 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
     }
     const float el2 = ex * ex + ey * ey + ez * ez;
-    for (int k = e0; k < e1; ++k) {
-      const float* E = sc.me32 + 16 * k;
+#pragma unroll 2
+    for (int k = B.e0; k < B.e1; ++k) {
+      const float* E = B.er + 16 * k;
       const float cx = E[0], cy = E[1], cz = E[2], dx = E[3], dy = E[4], dz = E[5];
       const float cba = cx * ux + cy * uy + cz * uz;
       const float dba = dx * ux + dy * uy + dz * uz;
@@ -133,8 +151,8 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
           float n0 = ey * fz - ez * fy, n1 = ez * fx - ex * fz, n2 = ex * fy - ey * fx;
           const float len2 = n0 * n0 + n1 * n1 + n2 * n2;
           const float fl2 = fx * fx + fy * fy + fz * fz;
-          if (len2 < 1e-4f * el2 * fl2) {
-            deg = true;  // nearly parallel edges: the axis direction needs fp64
+          if (!(len2 > 1e-4f * el2 * fl2)) {
+            deg = true;  // nearly parallel (or degenerate) edges: the axis needs fp64
           } else {
             const float il = rsqrtf(len2);
             const float ori = n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz);
@@ -146,21 +164,25 @@ __device__ __forceinline__ float exact_mesh_wave32(int link, const Pose pose, in
         }
       }
     }
-    if (base + 64 < le1 && !__ballot(deg)) {
+    if (base + 64 < A.e1 && !__ballot(deg)) {
       const float lf = fminf(pd, wave_minf(loc));
-      if (lf < P - kExactGuard) return lf;
+      if (lf < stop) { if (STAT) TCMP_MSTAT(10); return lf; }
     }
   }
-  if (__ballot(deg)) return __builtin_nanf("");
-  return fminf(pd, wave_minf(loc));
+  if (__ballot(deg)) { if (STAT) TCMP_MSTAT(13); return __builtin_nanf(""); }
+  const float res = fminf(pd, wave_minf(loc));
+  if (STAT) {
+    if (res >= (float)kPen) { TCMP_MSTAT(11); } else { TCMP_MSTAT(12); }
+  }
+  return res;
 }
 
-// fp64 restatement of exact_mesh_wave32 (same axes, strict Gauss-map test, no degeneracy
+// fp64 restatement of hull_hull_wave32 on the full hulls (same axes, strict Gauss-map test, no degeneracy
 // shortcuts): the decision-maker near kPen.  Every lane of the wave calls it.
 __device__ __noinline__ double exact_mesh_wave(int link, const Pose pose, int m, const Scene sc,
                                                const Geo g) {
   const int lane = lane_id();
-  const int* rg = sc.mrange + 8 * m;
+  const int* rg = sc.mrange + kMrange * m;
   const int v0 = rg[0], v1 = rg[1], f0 = rg[2], f1 = rg[3], e0 = rg[4], e1 = rg[5];
   const int lv0 = tcmp_geo_vert_off[link], lv1 = tcmp_geo_vert_off[link + 1];
   const int lf0 = tcmp_geo_plane_off[link], lf1 = tcmp_geo_plane_off[link + 1];

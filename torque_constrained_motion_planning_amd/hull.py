@@ -52,6 +52,40 @@ def hull_data(points):
     return v, np.array(planes, dtype=np.float64), np.array(edges, dtype=np.int32).reshape(-1, 4)
 
 
+def inner_lod(verts, k=24):
+    """Inner level of detail: the hull of k of the hull's vertices (a subset of the hull),
+    chosen greedily -- axis extremes first, then repeatedly the vertex farthest outside the
+    current subset hull.  Any penetration depth computed with it is <= the full hull's."""
+    from scipy.spatial import ConvexHull
+    v = np.asarray(verts, dtype=np.float64)
+    if len(v) <= k:
+        return hull_data(v)
+    idx = sorted({int(np.argmax(v @ d)) for d in np.vstack([np.eye(3), -np.eye(3)])})
+    while len(idx) < 4:
+        idx.append(next(i for i in range(len(v)) if i not in idx))
+    while len(idx) < k:
+        eq = ConvexHull(v[idx]).equations
+        d = (v @ eq[:, :3].T + eq[:, 3]).max(1)
+        j = int(np.argmax(d))
+        if d[j] <= 1e-12:
+            break
+        idx.append(j)
+    return hull_data(v[sorted(idx)])
+
+
+def outer_lod(verts, inner_planes):
+    """Outer level of detail: the H-polytope of the inner LOD's facet normals pushed out to
+    the full hull's support (a superset of the hull -- exactly, the planes are supports --
+    so depths computed with it are >= the full hull's), returned as the hull of its vertices
+    (hull_data: facets re-derived from those vertices, so containment holds by construction)."""
+    from scipy.spatial import HalfspaceIntersection
+    v = np.asarray(verts, dtype=np.float64)
+    n = inner_planes[:, :3] / np.linalg.norm(inner_planes[:, :3], axis=1)[:, None]
+    d = (v @ n.T).max(0)
+    hs = HalfspaceIntersection(np.hstack([n, -d[:, None]]), v.mean(0))
+    return hull_data(hs.intersections)
+
+
 def fit_boxes(verts, planes, n_random=300, seed=0):
     """Outer oriented box (contains the hull) and inner half extents (box of the same centre
     and axes inside the hull).  PCA axes refined over random rotations for a small volume;
@@ -112,36 +146,52 @@ class ConvexMesh:
         return (self.vertices * self.scale) @ self.rotation.T + self.position
 
     def record(self):
-        """(verts, planes, edges, box18) in the world frame; cached."""
+        """(verts, planes, edges, box18, inner LOD, outer LOD) in the world frame; cached.
+        The LODs are (verts, planes, edges) hulls inside / around the hull."""
         if self._rec is None:
             v, pl, e = hull_data(self.world_vertices())
             c, R, half, ih = fit_boxes(v, pl)
             box = np.concatenate([c, R.reshape(-1), half, ih])
-            self._rec = (v, pl, e, box)
+            inner = inner_lod(v)
+            outer = outer_lod(v, inner[1])
+            self._rec = (v, pl, e, box, inner, outer)
         return self._rec
 
     def __repr__(self):
         return "ConvexMesh(%s, %d verts, scale %.3g)" % (self.name, len(self.vertices), self.scale)
 
 
-class MeshPack:
-    """Flat arrays of tcmp_set_meshes (include/tcmp.h)."""
+class HullSet:
+    """Concatenated (verts, planes, edges) hulls with row offsets (struct tcmp_hulls)."""
+
+    def __init__(self, hulls):
+        self.verts = np.ascontiguousarray(np.concatenate([h[0] for h in hulls]) if hulls else np.zeros((0, 3)))
+        self.planes = np.ascontiguousarray(np.concatenate([h[1] for h in hulls]) if hulls else np.zeros((0, 4)))
+        self.edges = np.ascontiguousarray((np.concatenate([h[2] for h in hulls]) if hulls
+                                           else np.zeros((0, 4))).astype(np.int32))
+        self.vert_off = np.concatenate([[0], np.cumsum([len(h[0]) for h in hulls])]).astype(np.int32)
+        self.plane_off = np.concatenate([[0], np.cumsum([len(h[1]) for h in hulls])]).astype(np.int32)
+        self.edge_off = np.concatenate([[0], np.cumsum([len(h[2]) for h in hulls])]).astype(np.int32)
+
+    def arrays(self):
+        return (self.verts, self.vert_off, self.planes, self.plane_off, self.edges, self.edge_off)
+
+
+class MeshPack(HullSet):
+    """Flat arrays of tcmp_set_meshes (include/tcmp.h): the exact hulls, their boxes and the
+    inner / outer level-of-detail hulls (tcmp_set_mesh_lods)."""
 
     def __init__(self, meshes):
         recs = [m.record() for m in meshes]
+        HullSet.__init__(self, [r[:3] for r in recs])
         self.n = len(recs)
-        self.verts = np.ascontiguousarray(np.concatenate([r[0] for r in recs]) if recs else np.zeros((0, 3)))
-        self.planes = np.ascontiguousarray(np.concatenate([r[1] for r in recs]) if recs else np.zeros((0, 4)))
-        self.edges = np.ascontiguousarray((np.concatenate([r[2] for r in recs]) if recs
-                                           else np.zeros((0, 4))).astype(np.int32))
         self.boxes = np.ascontiguousarray(np.array([r[3] for r in recs]).reshape(-1, 18))
-        self.vert_off = np.concatenate([[0], np.cumsum([len(r[0]) for r in recs])]).astype(np.int32)
-        self.plane_off = np.concatenate([[0], np.cumsum([len(r[1]) for r in recs])]).astype(np.int32)
-        self.edge_off = np.concatenate([[0], np.cumsum([len(r[2]) for r in recs])]).astype(np.int32)
+        self.inner = HullSet([r[4] for r in recs])
+        self.outer = HullSet([r[5] for r in recs])
 
     def key(self):
-        return b"".join(a.tobytes() for a in (self.verts, self.planes, self.edges, self.boxes,
-                                              self.vert_off, self.plane_off, self.edge_off))
+        return b"".join(a.tobytes() for a in self.arrays() + (self.boxes,) + self.inner.arrays()
+                        + self.outer.arrays())
 
     def __len__(self):
         return self.n
