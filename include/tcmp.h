@@ -42,7 +42,7 @@ int tcmp_device_count(int* n);
 int tcmp_version(void);
 /* profiling builds (-DTCMP_PROF) only: k_edges clock breakdown accumulated since create
  * (total, work fetch, collision, torque, bookkeeping, tier-4 exact, ...) and exact-test
- * outcome counts (12..27), n <= 28; zeros otherwise. */
+ * outcome counts and mesh-stage clocks (12..35), n <= 36; zeros otherwise. */
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n);
 
 /* Fixed obstacles (replaces Problem.fixed bodies + pybullet getClosestPoints,

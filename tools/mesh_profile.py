@@ -20,7 +20,7 @@ def main():
     eng = _lib.Engine(0)
     obs, pack, goal = bench.make_query(1234, n_obs=0, n_mesh=W["meshes"], engine=eng)
     r, _ = bench.run_query(eng, obs, goal, n, W["batch"], 1234, meshes=pack)
-    c = eng.debug_counters(28)
+    c = eng.debug_counters(36)
     tot = max(1, c[0])
     print(json.dumps({"samples": n, "ms_edges": r.ms_edges, "ms_nearest": r.ms_nearest,
                       "edge_steps": r.edge_steps, "pairs_tested": r.pairs_tested,
@@ -33,7 +33,10 @@ def main():
                                      "inner_collision": c[18], "hull_hull_fp64": c[19]},
                       "hull_hull_exits": {"mesh_facets": c[20], "link_facets": c[21],
                                           "edges_early": c[22], "full_collision": c[23],
-                                          "full_free": c[24], "degenerate": c[25]}}),
+                                          "full_free": c[24], "degenerate": c[25]},
+                      "mesh_stage_clk_share": dict(zip(
+                          ("outer_box", "outer_lod", "inner_lod", "full_fp32", "fp64"),
+                          (round(x / max(1, sum(c[28:33])), 4) for x in c[28:33])))}),
           flush=True)
 
 

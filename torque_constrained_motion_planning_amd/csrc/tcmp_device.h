@@ -568,8 +568,9 @@ constexpr float kExactGuard = 1e-4f;
 #ifdef TCMP_PROF_EXACT
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
-__device__ unsigned long long g_exact_stats[16];  // [4..7]: mesh pairs (exact_pair),
-                                                  // [8..13]: exact_mesh_wave32 exits
+__device__ unsigned long long g_exact_stats[24];  // [4..7]: mesh pairs (exact_pair),
+                                                  // [8..13]: hull_hull_wave32 exits,
+                                                  // [16..20]: exact_pair mesh-stage clocks
 #endif
 __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g) {
@@ -712,12 +713,17 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
   }
 #ifdef TCMP_PROF_EXACT
 #define TCMP_MESH_STAT(i) if (lane_id() == 0) atomicAdd(&g_exact_stats[i], 1ull)
+  unsigned long long tclk = clock64();
+#define TCMP_MESH_CLK(i) { const unsigned long long t1 = clock64(); \
+    if (lane_id() == 0) atomicAdd(&g_exact_stats[16 + (i)], t1 - tclk); tclk = t1; }
 #else
 #define TCMP_MESH_STAT(i)
+#define TCMP_MESH_CLK(i)
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
   const float po = exact_pd_wave32(link, PL, ob, g);
+  TCMP_MESH_CLK(0);
   if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
   float R[9], p[3];
 #pragma unroll
@@ -733,6 +739,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
                      tcmp_lod_out_edge_off[link + 1]};
     const HullB32 Bo{sc.lv32[1], sc.lp32[1], sc.le32[1], rg[12], rg[13], rg[14], rg[15], rg[16], rg[17]};
     const float pl = hull_hull_wave32<false>(Ao, Bo, R, p, P - kExactGuard);
+    TCMP_MESH_CLK(1);
     if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); return (double)pl; }
     const HullA32 Ai{sc.lodv3[0], sc.lodpl[0], sc.lodei[0], sc.lodev[0], tcmp_lod_in_vert_off[link],
                      tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
@@ -740,6 +747,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
                      tcmp_lod_in_edge_off[link + 1]};
     const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11]};
     const float pi = hull_hull_wave32<false>(Ai, Bi, R, p, P + kExactGuard);
+    TCMP_MESH_CLK(2);
     if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
   } else {
     const double* ib = sc.mib + 16 * mi;
@@ -753,10 +761,14 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
                   tcmp_geo_plane_off[link + 1], tcmp_geo_edge_off[link], tcmp_geo_edge_off[link + 1]};
   const HullB32 B{sc.mv32, sc.mp32, sc.me32, rg[0], rg[1], rg[2], rg[3], rg[4], rg[5]};
   const float pm = hull_hull_wave32<true>(A, B, R, p, P - kExactGuard);
+  TCMP_MESH_CLK(3);
   if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;
   TCMP_MESH_STAT(7);
-  return exact_mesh_wave(link, PL, mi, sc, g);
+  const double r64 = exact_mesh_wave(link, PL, mi, sc, g);
+  TCMP_MESH_CLK(4);
+  return r64;
 #undef TCMP_MESH_STAT
+#undef TCMP_MESH_CLK
 }
 
 // ------------------------------------------------------------------------------------------

@@ -1162,15 +1162,15 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (int rc = set_dev(h)) return rc;
-  if (!out || n < 0 || n > 28) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 36) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   for (int i = 0; i < n; ++i) out[i] = s.prof[i];
 #ifdef TCMP_PROF_EXACT
-  unsigned long long ex[16];
+  unsigned long long ex[24];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
-  for (int i = 0; i < 16 && 12 + i < n; ++i) out[12 + i] = ex[i];
+  for (int i = 0; i < 24 && 12 + i < n; ++i) out[12 + i] = ex[i];
 #endif
   return 0;
 }

@@ -47,6 +47,76 @@ struct HullB32 {
   int v0, v1, f0, f1, e0, e1;
 };
 
+// Facet passes: lanes own 64*J facets, the other hull's vertices stream wave-uniformly;
+// returns this lane's minimum of (facet offset - support), INFINITY for empty slots.
+// BF: B's facets (moved into A's frame) against A's vertices; else A's facets (moved into
+// the world frame) against B's vertices.
+template <int J, bool BF>
+__device__ __forceinline__ float facet_pass32(const HullA32& A, const HullB32& B, const float R[9],
+                                              const float p[3], int base) {
+  const int lane = lane_id();
+  const int f1 = BF ? B.f1 : A.f1;
+  float nx[J], ny[J], nz[J], dd[J], mn[J];
+#pragma unroll
+  for (int j = 0; j < J; ++j) {
+    const int f = base + lane + 64 * j;
+    float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
+    if (f < f1) w = BF ? B.pl[f] : A.pl[f];
+    if (BF) {
+      nx[j] = R[0] * w.x + R[3] * w.y + R[6] * w.z;
+      ny[j] = R[1] * w.x + R[4] * w.y + R[7] * w.z;
+      nz[j] = R[2] * w.x + R[5] * w.y + R[8] * w.z;
+      dd[j] = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
+    } else {
+      nx[j] = R[0] * w.x + R[1] * w.y + R[2] * w.z;
+      ny[j] = R[3] * w.x + R[4] * w.y + R[5] * w.z;
+      nz[j] = R[6] * w.x + R[7] * w.y + R[8] * w.z;
+      dd[j] = w.w + (nx[j] * p[0] + ny[j] * p[1] + nz[j] * p[2]);
+    }
+    mn[j] = INFINITY;
+  }
+  if (BF) {
+    for (int v = A.v0; v < A.v1; ++v) {
+      const float x = A.v3[3 * v], y = A.v3[3 * v + 1], z = A.v3[3 * v + 2];
+#pragma unroll
+      for (int j = 0; j < J; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
+    }
+  } else {
+    for (int v = B.v0; v < B.v1; ++v) {
+      const float4 P4 = B.v[v];
+#pragma unroll
+      for (int j = 0; j < J; ++j) mn[j] = fminf(mn[j], nx[j] * P4.x + ny[j] * P4.y + nz[j] * P4.z);
+    }
+  }
+  float loc = INFINITY;
+#pragma unroll
+  for (int j = 0; j < J; ++j) loc = fminf(loc, dd[j] - mn[j]);
+  return loc;
+}
+
+// All facets of one hull in passes of 256 / 128 / 64 (so a hull of <= 64 facets costs one
+// vertex stream with one facet per lane).
+template <bool BF>
+__device__ __forceinline__ float facets32(const HullA32& A, const HullB32& B, const float R[9],
+                                          const float p[3]) {
+  const int f0 = BF ? B.f0 : A.f0, f1 = BF ? B.f1 : A.f1;
+  float loc = INFINITY;
+  for (int base = f0; base < f1;) {
+    const int rem = f1 - base;
+    if (rem > 128) {
+      loc = fminf(loc, facet_pass32<4, BF>(A, B, R, p, base));
+      base += 256;
+    } else if (rem > 64) {
+      loc = fminf(loc, facet_pass32<2, BF>(A, B, R, p, base));
+      base += 128;
+    } else {
+      loc = fminf(loc, facet_pass32<1, BF>(A, B, R, p, base));
+      base += 64;
+    }
+  }
+  return loc;
+}
+
 // fp32 penetration depth of hull A (pose R, p) against hull B, wave-cooperative.  Returns as
 // soon as a stage's minimum falls below `stop` (then the value is only an upper bound below
 // `stop`), NaN when an edge axis is too degenerate for fp32 (see the header comment).
@@ -54,55 +124,13 @@ template <bool STAT>
 __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32 B,
                                                   const float R[9], const float p[3], float stop) {
   const int lane = lane_id();
-  float loc = INFINITY;
   // (1) B's facets (moved into A's frame) against A's vertices (uniform stream)
-  for (int base = B.f0; base < B.f1; base += 256) {
-    float nx[4], ny[4], nz[4], dd[4], mn[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = base + lane + 64 * j;
-      float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
-      if (f < B.f1) w = B.pl[f];
-      nx[j] = R[0] * w.x + R[3] * w.y + R[6] * w.z;
-      ny[j] = R[1] * w.x + R[4] * w.y + R[7] * w.z;
-      nz[j] = R[2] * w.x + R[5] * w.y + R[8] * w.z;
-      dd[j] = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
-      mn[j] = INFINITY;
-    }
-    for (int v = A.v0; v < A.v1; ++v) {
-      const float x = A.v3[3 * v], y = A.v3[3 * v + 1], z = A.v3[3 * v + 2];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
-  }
-  float pd = wave_minf(loc);
+  float pd = wave_minf(facets32<true>(A, B, R, p));
   if (pd < stop) { if (STAT) TCMP_MSTAT(8); return pd; }
   // (2) A's facets (moved into the world frame) against B's vertices
-  for (int base = A.f0; base < A.f1; base += 256) {
-    float nx[4], ny[4], nz[4], dd[4], mn[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int f = base + lane + 64 * j;
-      float4 w = make_float4(0.f, 0.f, 0.f, INFINITY);
-      if (f < A.f1) w = A.pl[f];
-      nx[j] = R[0] * w.x + R[1] * w.y + R[2] * w.z;
-      ny[j] = R[3] * w.x + R[4] * w.y + R[5] * w.z;
-      nz[j] = R[6] * w.x + R[7] * w.y + R[8] * w.z;
-      dd[j] = w.w + (nx[j] * p[0] + ny[j] * p[1] + nz[j] * p[2]);
-      mn[j] = INFINITY;
-    }
-    for (int v = B.v0; v < B.v1; ++v) {
-      const float4 P4 = B.v[v];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) mn[j] = fminf(mn[j], nx[j] * P4.x + ny[j] * P4.y + nz[j] * P4.z);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) loc = fminf(loc, dd[j] - mn[j]);
-  }
-  pd = fminf(pd, wave_minf(loc));
+  pd = fminf(pd, wave_minf(facets32<false>(A, B, R, p)));
   if (pd < stop) { if (STAT) TCMP_MSTAT(9); return pd; }
+  float loc = INFINITY;
   // (3) edge pairs: lanes own A's edges, B's edges stream wave-uniformly
   bool deg = false;
   for (int base = A.e0; base < A.e1; base += 64) {
