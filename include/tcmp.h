@@ -85,6 +85,15 @@ typedef struct tcmp_hulls {
 int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls* outer,
                        int32_t n_mesh);
 
+/* Self-collision (get_collision_fn(..., self_collisions=True), utils.py:3165-3191 with the
+ * pairs of get_self_link_pairs, utils.py:3125-3149): enable != 0 adds the 33 link pairs of
+ * the arm whose moving-ancestor joint sets differ and that are not parent/child (link0 is the
+ * base, outside get_links; link8 has no geometry), same -0.04 closest-point threshold
+ * (pairwise_link_collision -> get_closest_points default, utils.py:2781,2833,2851).  Every
+ * later collision check (configs, edges, planning rounds, rewiring) includes them.  Off by
+ * default, as in the reference planner (SELF_COLLISIONS = False, utils.py:56). */
+int tcmp_set_self_collision(tcmp_handle* h, int32_t enable);
+
 /* ---- batched physics (host arrays in/out) ---------------------------------------------- */
 /* rne(q, qd, qdd) with add_payload(r, m) state made explicit: payload iff payload_mass > 0
  * (rne.py:181-254).  q, qd, qdd, tau: n x 7. */

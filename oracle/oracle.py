@@ -64,6 +64,10 @@ def lib():
         L.orc_set_meshes.argtypes = [_dp, _ip, _dp, _ip, _ip, _ip, _dp, ctypes.c_int]
         L.orc_mesh_pair_pd.argtypes = [ctypes.c_int, _dp, ctypes.c_int, ctypes.c_int]
         L.orc_mesh_pair_pd.restype = ctypes.c_double
+        L.orc_set_self_collision.argtypes = [ctypes.c_int]
+        L.orc_self_pairs.argtypes = [_ip]
+        L.orc_self_pair_pd.argtypes = [ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int]
+        L.orc_self_pair_pd.restype = ctypes.c_double
         L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
                                   ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
         assert L.orc_sizeof_cfg() == ctypes.sizeof(RrtCfg), "oracle cfg layout mismatch"
@@ -167,6 +171,25 @@ def set_meshes(pack):
     ip = lambda a: a.ctypes.data_as(_ip)  # noqa: E731
     L.orc_set_meshes(_d(arrs[0]), ip(arrs[1]), _d(arrs[2]), ip(arrs[3]), ip(arrs[4]),
                      ip(arrs[5]), _d(arrs[6]), int(pack.n))
+
+
+def set_self_collision(on):
+    """Self-collision pairs on/off for every later collision / check_edge / rrt_run call
+    (module-level state of the oracle library)."""
+    lib().orc_set_self_collision(int(bool(on)))
+
+
+def self_pairs():
+    """Collision-link index pairs of get_self_link_pairs (utils.py:3138-3149), restated."""
+    out = np.zeros(2 * 66, dtype=np.intc)
+    n = lib().orc_self_pairs(out.ctypes.data_as(_ip))
+    return [tuple(int(x) for x in out[2 * i:2 * i + 2]) for i in range(n)]
+
+
+def self_pair_pd(a, b, q, method=0):
+    """Penetration depth of link hulls a, b at q; method 0 brute force, 1 Gauss-map."""
+    q = _arr(q, (7,))
+    return lib().orc_self_pair_pd(int(a), int(b), _d(q), int(method))
 
 
 def mesh_pair_pd(link, q, m, method=0):

@@ -748,15 +748,9 @@ static void proj_range(const double* v, int nv, const double n[3], double* mn, d
  * edge pair cross product), both directions, supports from all vertices.  The minimum
  * overlap is the penetration depth (each candidate overlap is >= it and the facet normals of
  * the Minkowski difference are among the candidates).  O(E_A E_B (V_A + V_B)). */
-ORC_API double orc_hull_mesh_pd_brute(int link, const double* fr, int m) {
-  static orc_whull A;
-  link_world_hull(link, fr, &A);
-  const double* Bv = g_mesh.v + 3 * g_mesh.voff[m];
-  const int nvb = g_mesh.voff[m + 1] - g_mesh.voff[m];
-  const double* Bp = g_mesh.pl + 4 * g_mesh.poff[m];
-  const int nfb = g_mesh.poff[m + 1] - g_mesh.poff[m];
-  const int* Be = g_mesh.e + 4 * g_mesh.eoff[m];
-  const int neb = g_mesh.eoff[m + 1] - g_mesh.eoff[m];
+static double hull_pd_brute(const orc_whull* Ap, const double* Bv, int nvb, const double* Bp,
+                            int nfb, const int* Be, int neb) {
+  const orc_whull A = *Ap;
   double pd = INFINITY;
   for (int pass = 0; pass < 2; ++pass) {
     const double* pl = pass ? Bp : A.pl;
@@ -795,20 +789,22 @@ ORC_API double orc_hull_mesh_pd_brute(int link, const double* fr, int m) {
   return pd;
 }
 
+ORC_API double orc_hull_mesh_pd_brute(int link, const double* fr, int m) {
+  static orc_whull A;
+  link_world_hull(link, fr, &A);
+  return hull_pd_brute(&A, g_mesh.v + 3 * g_mesh.voff[m], g_mesh.voff[m + 1] - g_mesh.voff[m],
+                       g_mesh.pl + 4 * g_mesh.poff[m], g_mesh.poff[m + 1] - g_mesh.poff[m],
+                       g_mesh.e + 4 * g_mesh.eoff[m], g_mesh.eoff[m + 1] - g_mesh.eoff[m]);
+}
+
 /* Same depth over the Minkowski-difference facets only: facets of B against A's vertices,
  * facets of A against B's vertices, and the edge pairs whose Gauss-map arcs intersect
  * (a, b = A's adjacent facet normals; c, d = B's negated), with the support read off the
  * edge points.  Mathematically identical to the brute force when the result is >= 0; the
  * GPU's fp64 pass (csrc/tcmp_mesh.h exact_mesh_wave) is this computation. */
-ORC_API double orc_hull_mesh_pd_gauss(int link, const double* fr, int m) {
-  static orc_whull A;
-  link_world_hull(link, fr, &A);
-  const double* Bv = g_mesh.v + 3 * g_mesh.voff[m];
-  const int nvb = g_mesh.voff[m + 1] - g_mesh.voff[m];
-  const double* Bp = g_mesh.pl + 4 * g_mesh.poff[m];
-  const int nfb = g_mesh.poff[m + 1] - g_mesh.poff[m];
-  const int* Be = g_mesh.e + 4 * g_mesh.eoff[m];
-  const int neb = g_mesh.eoff[m + 1] - g_mesh.eoff[m];
+static double hull_pd_gauss(const orc_whull* Ap, const double* Bv, int nvb, const double* Bp,
+                            int nfb, const int* Be, int neb) {
+  const orc_whull A = *Ap;
   double pd = INFINITY;
   for (int f = 0; f < nfb; ++f) {
     double amn, amx;
@@ -853,6 +849,95 @@ ORC_API double orc_hull_mesh_pd_gauss(int link, const double* fr, int m) {
   return pd;
 }
 
+ORC_API double orc_hull_mesh_pd_gauss(int link, const double* fr, int m) {
+  static orc_whull A;
+  link_world_hull(link, fr, &A);
+  return hull_pd_gauss(&A, g_mesh.v + 3 * g_mesh.voff[m], g_mesh.voff[m + 1] - g_mesh.voff[m],
+                       g_mesh.pl + 4 * g_mesh.poff[m], g_mesh.poff[m + 1] - g_mesh.poff[m],
+                       g_mesh.e + 4 * g_mesh.eoff[m], g_mesh.eoff[m + 1] - g_mesh.eoff[m]);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* self-collision pairs (get_collision_fn self_collisions=True, utils.py:3165-3191)        */
+/* ------------------------------------------------------------------------------------ */
+/* The links pybullet lists for the panda body (get_links: children of joints, in joint order;
+ * panda_mod.urdf), their parent link (-1 = base link0), whether the joint above them is one
+ * of the 7 arm joints planned over, and their collision-link index (-1 = no geometry). */
+enum { ORC_BODY_LINKS = 12 };
+static const int kBodyParent[ORC_BODY_LINKS] = {-1, 0, 1, 2, 3, 4, 5, 6, 7, 8, 8, 8};
+static const int kBodyArmJoint[ORC_BODY_LINKS] = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 0, 0};
+/* link1..link7, link8, hand, leftfinger, rightfinger, grasptarget */
+static const int kBodyColl[ORC_BODY_LINKS] = {0, 1, 2, 3, 4, 5, 6, -1, 7, 8, 9, -1};
+
+static int g_self = 0;
+ORC_API void orc_set_self_collision(int on) { g_self = on ? 1 : 0; }
+
+/* moving arm joints among a link's ancestors, itself included (get_joint_ancestors & joints) */
+static unsigned arm_ancestors(int l) {
+  unsigned m = 0;
+  for (; l >= 0; l = kBodyParent[l])
+    if (kBodyArmJoint[l]) m |= 1u << l;
+  return m;
+}
+
+/* get_self_link_pairs(only_moving=True, disabled=set()) (utils.py:3138-3149): every moving
+ * link is a child of an arm joint's subtree, so fixed_links is empty (the base is not in
+ * get_links); get_moving_pairs (:3125-3136) keeps pairs whose ancestor sets differ; adjacent
+ * (parent/child, :1766) pairs are dropped; links without collision shapes give no closest
+ * points (pairwise_link_collision is False).  Writes collision-link index pairs. */
+ORC_API int orc_self_pairs(int* out) {
+  int n = 0;
+  for (int a = 0; a < ORC_BODY_LINKS; ++a)
+    for (int b = a + 1; b < ORC_BODY_LINKS; ++b) {
+      if (arm_ancestors(a) == arm_ancestors(b)) continue;
+      if (kBodyParent[a] == b || kBodyParent[b] == a) continue;
+      if (kBodyColl[a] < 0 || kBodyColl[b] < 0) continue;
+      if (out) { out[2 * n] = kBodyColl[a]; out[2 * n + 1] = kBodyColl[b]; }
+      ++n;
+    }
+  return n;
+}
+
+/* link a (frame fa) vs link b (frame fb): outer-OBB SAT (free) and inner-box SAT (collision)
+ * first when cull, then the exact hull-vs-hull depth (Gauss-map for cull == 2, else brute) */
+static int orc_self_pair_collides(int a, const double* fa, int b, const double* fb, int cull) {
+  if (cull) {
+    const double* ba = tcmp_geo_boxes + 18 * a;
+    const double* bb = tcmp_geo_boxes + 18 * b;
+    double wb[18]; /* link b's box record in the world frame: c, B (columns = axes), h, inner h */
+    for (int i = 0; i < 3; ++i) {
+      wb[i] = fb[9 + i];
+      for (int k = 0; k < 3; ++k) wb[i] += fb[3 * i + k] * bb[k];
+      for (int j = 0; j < 3; ++j) {
+        wb[3 + 3 * i + j] = 0.0;
+        for (int k = 0; k < 3; ++k) wb[3 + 3 * i + j] += fb[3 * i + k] * bb[3 + 3 * k + j];
+      }
+    }
+    for (int k = 12; k < 18; ++k) wb[k] = bb[k];
+    double cl[3], A[9];
+    box_to_link(fa, wb, cl, A);
+    if (obb_obb_pd(ba, ba + 3, ba + 12, cl, A, wb + 12) < ORC_PEN) return 0;
+    if (ba[15] > 0 && bb[15] > 0 && obb_obb_pd(ba, ba + 3, ba + 15, cl, A, wb + 15) >= ORC_PEN) return 1;
+  }
+  static orc_whull A, B;
+  link_world_hull(a, fa, &A);
+  link_world_hull(b, fb, &B);
+  const double pd = cull == 2 ? hull_pd_gauss(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne)
+                              : hull_pd_brute(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne);
+  return pd >= ORC_PEN;
+}
+
+/* depth of self pair (a, b) at q: method 0 brute force, 1 Gauss-map */
+ORC_API double orc_self_pair_pd(int a, int b, const double* q, int method) {
+  double fr[120];
+  orc_fk_links(q, fr);
+  static orc_whull A, B;
+  link_world_hull(a, fr + 12 * a, &A);
+  link_world_hull(b, fr + 12 * b, &B);
+  return method == 1 ? hull_pd_gauss(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne)
+                     : hull_pd_brute(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne);
+}
+
 /* link (frame fr) vs mesh m: cull = outer-box SAT (free) / inner-box SAT (collision) first;
  * cull == 2 then runs the Gauss-map test, otherwise the brute force.  Same answer. */
 static int orc_mesh_pair_collides(int link, const double* fr, int m, int cull, long* n_exact) {
@@ -878,13 +963,22 @@ ORC_API double orc_mesh_pair_pd(int link, const double* q, int m, int method) {
 }
 
 /* collision_fn (utils.py:3165-3218): limits first, then every moving link x obstacle.
- * Self-collision off (utils.py:56 SELF_COLLISIONS=False), no attachments.  Convex meshes
+ * Self-collision pairs only after orc_set_self_collision(1) (off in the reference planner,
+ * utils.py:56 SELF_COLLISIONS=False), no attachments.  Convex meshes
  * (orc_set_meshes) after the boxes. */
 ORC_API int orc_collision(const double* q, const double* obs, int n_obs, int cull) {
   if (orc_limits_violated(q)) return 1;
-  if (n_obs <= 0 && g_mesh.n <= 0) return 0;
+  if (n_obs <= 0 && g_mesh.n <= 0 && !g_self) return 0;
   double fr[120];
   orc_fk_links(q, fr);
+  if (g_self) {
+    int pr[2 * 66];
+    const int np = orc_self_pairs(pr);
+    for (int i = 0; i < np; ++i)
+      if (orc_self_pair_collides(pr[2 * i], fr + 12 * pr[2 * i], pr[2 * i + 1],
+                                 fr + 12 * pr[2 * i + 1], cull))
+        return 1;
+  }
   for (int l = 0; l < TCMP_NLINKS; ++l)
     for (int o = 0; o < n_obs; ++o)
       if (orc_pair_collides(l, fr + 12 * l, obs + 15 * o, cull, 0)) return 1;

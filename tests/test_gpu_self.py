@@ -1,0 +1,137 @@
+"""GPU parity for self-collision pairs (get_collision_fn(...,
+self_collisions=True), utils.py:3165-3191, pairs of get_self_link_pairs, utils.py:3138-3149)
+against the CPU oracle's restatement: flags, edge safe prefixes and batched RRT* trees exact,
+alone and combined with box and convex-mesh obstacles.  The reference planner runs with
+SELF_COLLISIONS = False (utils.py:56), so these paths are opt-in; parity against Bullet is
+unpinned, as for every collision result (pybullet is absent).
+"""
+import numpy as np
+import pytest
+
+import oracle as O  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+START = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from torque_constrained_motion_planning_amd import _lib
+    e = _lib.engine(0)
+    yield e
+    e.set_self_collision(False)
+
+
+@pytest.fixture(autouse=True)
+def _reset_oracle():
+    yield
+    O.set_self_collision(False)
+    O.set_meshes(None)
+
+
+def rand_q(rng, n):
+    return LO + (HI - LO) * rng.random((n, 7))
+
+
+def test_self_collision_flags_vs_oracle(eng):
+    rng = np.random.default_rng(11)
+    q = rand_q(rng, 2500)
+    eng.set_scene(np.zeros((0, 15)))
+    eng.set_self_collision(True)
+    O.set_self_collision(True)
+    got = eng.collides(q)
+    ref = np.array([O.collision(x, None, cull=2) for x in q])
+    assert (got == ref).all(), np.nonzero(got != ref)
+    assert 0 < got.sum() < len(q)  # both answers exercised (~4 % self-collide)
+    # off again: only the joint limits remain in an empty scene
+    eng.set_self_collision(False)
+    assert not eng.collides(q).any()
+
+
+def test_self_collision_near_threshold(eng):
+    """Configurations with a self pair within 2 cm of the 0.04 m threshold, against the
+    oracle's brute-force depth (the fp32 pass defers to fp64 there)."""
+    rng = np.random.default_rng(12)
+    pairs = O.self_pairs()
+    q = rand_q(rng, 2000)
+    near = []
+    for x in q:
+        d = max(O.self_pair_pd(a, b, x, 1) for a, b in pairs)
+        if abs(d - 0.04) < 0.02:
+            near.append(x)
+        if len(near) == 25:
+            break
+    assert len(near) >= 10
+    near = np.array(near)
+    eng.set_scene(np.zeros((0, 15)))
+    eng.set_self_collision(True)
+    got = eng.collides(near)
+    ref = np.array([max(O.self_pair_pd(a, b, x, 0) for a, b in pairs) >= 0.04 for x in near])
+    assert (got == ref).all()
+
+
+def test_self_collision_with_obstacles_vs_oracle(eng):
+    from torque_constrained_motion_planning_amd.scene import (mesh_pack, obstacle_array,
+                                                               random_box_scene,
+                                                               random_mesh_scene)
+    rng = np.random.default_rng(13)
+    obs = obstacle_array(random_box_scene(rng, 6))
+    ms = random_mesh_scene(rng, 6)
+    pack = mesh_pack(ms)
+    q = rand_q(rng, 1000)
+    O.set_self_collision(True)
+    for scene_obs, scene_pack in ((obs, None), (np.zeros((0, 15)), pack), (obs, pack)):
+        eng.set_scene(scene_obs, scene_pack)
+        eng.set_self_collision(True)
+        O.set_meshes(scene_pack)
+        got = eng.collides(q)
+        ref = np.array([O.collision(x, scene_obs, cull=2) for x in q])
+        assert (got == ref).all(), np.nonzero(got != ref)
+
+
+def test_self_collision_edges_vs_oracle(eng):
+    rng = np.random.default_rng(14)
+    eng.set_scene(np.zeros((0, 15)))
+    eng.set_self_collision(True)
+    O.set_self_collision(True)
+    a = np.repeat(START[None], 400, 0)
+    a[200:] = rand_q(rng, 200)
+    b = rand_q(rng, 400)
+    ns, nt, last = eng.check_edges(a, b, 2, 5.0)
+    cut = 0
+    for i in range(len(a)):
+        s, n, l = O.check_edge(a[i], b[i], None, 2, 5.0, cull=2)
+        assert ns[i] == s and nt[i] == n, (i, ns[i], s, nt[i], n)
+        if s:
+            assert np.array_equal(last[i], l), i
+        cut += s < n
+    assert cut > 0
+
+
+@pytest.mark.parametrize("batch", [1, 256])
+def test_self_collision_batched_frontier_vs_oracle(eng, batch):
+    from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    rng = np.random.default_rng(400 + batch)
+    O.set_self_collision(True)
+    goal = None
+    while goal is None:
+        g = rand_q(rng, 1)[0]
+        if not O.collision(g, None, cull=2) and O.torque_ok(g, 2, 5.0):
+            goal = g
+    n_samples = 3 * batch + 17 if batch > 1 else 60
+    (path, vels, accels, psg), r, raw = rrt_star_batched(
+        START, goal, [], 2, 5.0, 1.0, n_samples, batch=batch, seed=7 + batch, engine=eng,
+        self_collisions=True)
+    ref = O.rrt_run(START, goal, n_samples, None, 2, 5.0, 1.0, batch=batch, seed=7 + batch,
+                    cull=2)
+    assert r.n_nodes == ref["n_nodes"]
+    assert r.edge_steps == ref["edge_steps"]
+    assert r.goal_node == ref["goal_node"]
+    assert r.status == ref["status"]
+    if ref["status"] in (0, 3):
+        assert r.n_waypoints == ref["n_waypoints"]
+        assert np.abs(raw["waypoints"] - ref["waypoints"]).max() < 1e-12
+        assert np.abs(raw["q"] - ref["q"]).max() < 1e-9

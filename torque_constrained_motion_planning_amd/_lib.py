@@ -23,7 +23,7 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 # C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
-    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk", "tcmp_debug_counters",
@@ -94,6 +94,7 @@ def load_library(path=LIB_PATH):
         L.tcmp_set_meshes.argtypes = [vp, _dp, _i32p, _dp, _i32p, _i32p, _i32p, _dp, ctypes.c_int32]
         L.tcmp_set_mesh_lods.argtypes = [vp, ctypes.POINTER(Hulls), ctypes.POINTER(Hulls),
                                          ctypes.c_int32]
+        L.tcmp_set_self_collision.argtypes = [vp, ctypes.c_int32]
         L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
                                      ctypes.c_double, _i32p]
@@ -150,6 +151,7 @@ class Engine:
         self.device = device
         self._scene_key = None
         self._mesh_key = b""
+        self._self_coll = False
 
     def _check(self, rc):
         if rc != 0:
@@ -247,6 +249,13 @@ class Engine:
         self._check(self.L.tcmp_torque_ok(self.h, _d(q), _d(qd), _d(qdd), len(q), int(mode),
                                           float(mass), ok.ctypes.data_as(_i32p)))
         return ok.astype(bool)
+
+    def set_self_collision(self, enable):
+        """Self-collision pairs on/off for every later check (tcmp_set_self_collision)."""
+        enable = bool(enable)
+        if enable != self._self_coll:
+            self._check(self.L.tcmp_set_self_collision(self.h, int(enable)))
+            self._self_coll = enable
 
     def collides(self, q):
         q = _rows(q, "q")

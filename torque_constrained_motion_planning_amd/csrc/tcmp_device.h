@@ -116,6 +116,11 @@ struct Scene {
   // difference of nearby vertices would lose the direction of short edges)
   const float4* lodev[2];
   const float4* geo_ev;
+  // self-collision pairs (tcmp_set_self_collision): the 10 link hulls are appended to the
+  // mesh arrays as meshes n_mesh + j in their own link frames, and their outer-box records
+  // follow the obstacles (obs rows n_obs + j, not in tier 0's obstacle loop)
+  int n_mesh;
+  int self_coll;
 };
 constexpr int kMrange = 24;  // ints per mesh in Scene::mrange
 __device__ __forceinline__ int obs_mesh(const double* ob) {
@@ -931,6 +936,19 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
   return inner_all ? 1 : 2;
 }
 
+// Self-collision pairs of get_self_link_pairs(panda, arm joints) (utils.py:3125-3149):
+// links whose sets of moving ancestor joints differ (get_moving_pairs), minus parent/child
+// pairs (are_links_adjacent, utils.py:1766); link7, link8, the hand and the fingers share the
+// ancestor set {joint1..joint7}, link0 is the base (not in get_links), link8 has no geometry.
+// Pair p checks link kSelfA[p] against link kSelfB[p] (link indices of the collision links).
+constexpr int kNumSelfPairs = 33;
+__device__ constexpr int kSelfA[kNumSelfPairs] = {
+    0, 0, 0, 0, 0, 1, 1, 1, 1, 2, 2, 2, 3, 3, 4,
+    0, 0, 0, 1, 1, 1, 2, 2, 2, 3, 3, 3, 4, 4, 4, 5, 5, 5};
+__device__ constexpr int kSelfB[kNumSelfPairs] = {
+    2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6,
+    7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9};
+
 // Returns collision flag; all lanes must call.  `active` lanes only contribute.
 //
 // Phase A (every step): the 10 link frames are generated incrementally and each link's world
@@ -998,7 +1016,7 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
                                               const double sq[7], bool active,
                                               const Scene sc, const Geo g, StepStats& st) {
   bool coll = active && limits_violated(q);
-  if (sc.n_obs == 0) return coll;
+  if (sc.n_obs == 0 && !(MESH && sc.self_coll)) return coll;
   const int lane = lane_id();
   unsigned* queue = sc.wq;
   unsigned long long* cmask = reinterpret_cast<unsigned long long*>(sc.wq + kQcap);
@@ -1024,11 +1042,32 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
       }
       double R[9], p[3];
       link_pose(lk, c, s, R, p);
+      // obstacle record row: the obstacle, or for a self pair the other link's outer box in
+      // its own frame (row n_obs + j) -- the pose then becomes lk's pose in link j's frame
+      int orow = o;
+      if (MESH && o >= sc.n_obs) {
+        const int j = kSelfB[o - sc.n_obs];
+        orow = sc.n_obs + j;
+        double Rj[9], pj[3];
+        link_pose(j, c, s, Rj, pj);
+        double Rr[9], pr[3];
+#pragma unroll
+        for (int a = 0; a < 3; ++a) {
+#pragma unroll
+          for (int b = 0; b < 3; ++b)
+            Rr[3 * a + b] = Rj[a] * R[b] + Rj[3 + a] * R[3 + b] + Rj[6 + a] * R[6 + b];
+          pr[a] = Rj[a] * (p[0] - pj[0]) + Rj[3 + a] * (p[1] - pj[1]) + Rj[6 + a] * (p[2] - pj[2]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) R[k] = Rr[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) p[k] = pr[k];
+      }
       int cls = 0;
       if (has) {
         double wc[3], U[9], aabb[3];
         link_obb(lk, R, p, wc, U, aabb);
-        const double* ob = sc.obs + 16 * o;
+        const double* ob = sc.obs + 16 * orow;
         const int mi = MESH ? obs_mesh(ob) : -1;
         cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, st);
       }
@@ -1040,7 +1079,7 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
         const int sL = __shfl(src, L);
         __builtin_amdgcn_wave_barrier();
         if ((*cmask >> sL) & 1ull) continue;  // that lane already collides
-        const int lL = __shfl(lk, L), oL = __shfl(o, L);
+        const int lL = __shfl(lk, L), oL = __shfl(orow, L);
         Pose PL;
 #pragma unroll
         for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
@@ -1112,17 +1151,36 @@ __device__ __forceinline__ bool collides_wave(const double q[7], const double cq
       frame_step(R, p, I, tr);
       put(9, R, p);
     }
+    // self pairs whose link AABBs overlap by kPen on all three axes (tier 0 of a self pair;
+    // bh carries the rounding margin of both boxes)
+    uint64_t smask = 0;
+    if (MESH && sc.self_coll) {
+      constexpr float P = (float)kPen;
+#pragma unroll
+      for (int q = 0; q < kNumSelfPairs; ++q) {
+        const int a = kSelfA[q], b = kSelfB[q];
+        smask |= (uint64_t)((int)(fabsf(bc[a][0] - bc[b][0]) <= bh[a][0] + bh[b][0] - P) &
+                            (int)(fabsf(bc[a][1] - bc[b][1]) <= bh[a][1] + bh[b][1] - P) &
+                            (int)(fabsf(bc[a][2] - bc[b][2]) <= bh[a][2] + bh[b][2] - P)) << q;
+      }
+    }
+    const int n_tier0 = sc.n_obs + ((MESH && sc.self_coll) ? kNumSelfPairs : 0);
     // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
     bool full = false;
-    for (int o = o_res; o < sc.n_obs && !full; ++o) {
-      const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
-      const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
+    for (int o = o_res; o < n_tier0 && !full; ++o) {
       unsigned lm = 0;
+      if (o < sc.n_obs) {
+        const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
+        const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
 #pragma unroll
-      for (int l = 0; l < 10; ++l)
-        lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
-                         (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
-                         (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
+        for (int l = 0; l < 10; ++l)
+          lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
+                           (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
+                           (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
+      } else if (MESH) {
+        const int q = o - sc.n_obs;
+        lm = (unsigned)((smask >> q) & 1ull) << kSelfA[q];
+      }
       if (!live) lm = 0;
       if (o == o_res) lm &= ~((1u << l_res) - 1u);  // links already queued before a flush
       if (__ballot(lm != 0u) == 0) continue;

@@ -879,6 +879,8 @@ struct tcmp_handle {
   // obstacle list is the boxes followed by the meshes' outer boxes
   std::vector<double> box15;
   int n_box = 0, n_mesh = 0;
+  int self_coll = 0;  // tcmp_set_self_collision: link hulls appended as meshes n_mesh + j
+  bool mesh_kernels() const { return n_mesh > 0 || self_coll; }
   std::vector<double> mesh_v, mesh_p, mesh_box;
   std::vector<int> mesh_e, mesh_voff, mesh_poff, mesh_eoff;
   DBuf<int> mrange;
@@ -956,6 +958,8 @@ struct tcmp_handle {
       s.lodev[i] = reinterpret_cast<const float4*>(lodev[i].p);
     }
     s.geo_ev = reinterpret_cast<const float4*>(geo_ev.p);
+    s.n_mesh = n_mesh;
+    s.self_coll = self_coll;
     return s;
   }
 
@@ -1012,7 +1016,7 @@ int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
 }
 
 unsigned lds_bytes(const tcmp_handle* h) {
-  return h->n_mesh ? stage_lds_bytes_lean(h->n_obs) : stage_lds_bytes(h->n_obs);
+  return h->mesh_kernels() ? stage_lds_bytes_lean(h->n_obs) : stage_lds_bytes(h->n_obs);
 }
 
 unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>(1, (n + block - 1) / block); }
@@ -1130,7 +1134,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(h->n_mesh ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, P,
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, P,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1372,9 +1376,87 @@ int check_hulls(const tcmp_hulls* H, int n, const char* what) {
   return 0;
 }
 
+// Device mesh arrays from the host copies: the user meshes, then (self-collision on) the 10
+// link hulls in their own link frames as meshes n_mesh + j.  keep_lods: the user meshes'
+// level-of-detail rows (tcmp_set_mesh_lods) survive the rebuild.
+int upload_meshes(tcmp_handle* h, bool keep_lods) {
+  const int n_user = h->n_mesh, n_self = h->self_coll ? TCMP_NLINKS : 0;
+  const int n_mesh = n_user + n_self;
+  std::vector<double> verts(h->mesh_v), planes(h->mesh_p), boxes(h->mesh_box);
+  std::vector<int> edges(h->mesh_e), vert_off(h->mesh_voff), plane_off(h->mesh_poff),
+      edge_off(h->mesh_eoff);
+  if (vert_off.empty()) vert_off.assign(1, 0);
+  if (plane_off.empty()) plane_off.assign(1, 0);
+  if (edge_off.empty()) edge_off.assign(1, 0);
+  for (int j = 0; j < n_self; ++j) {
+    const int v0 = tcmp_geo_vert_off[j], f0 = tcmp_geo_plane_off[j];
+    for (int v = v0; v < tcmp_geo_vert_off[j + 1]; ++v)
+      for (int k = 0; k < 3; ++k) verts.push_back(tcmp_geo_verts[4 * v + k]);
+    for (int f = f0; f < tcmp_geo_plane_off[j + 1]; ++f)
+      for (int k = 0; k < 4; ++k) planes.push_back(tcmp_geo_planes[8 * f + k]);
+    for (int e = tcmp_geo_edge_off[j]; e < tcmp_geo_edge_off[j + 1]; ++e) {
+      const unsigned short* q = tcmp_geo_edge_idx + 4 * e;
+      edges.push_back(q[0] - v0); edges.push_back(q[1] - v0);
+      edges.push_back(q[2] - f0); edges.push_back(q[3] - f0);
+    }
+    for (int k = 0; k < 18; ++k) boxes.push_back(tcmp_geo_boxes[18 * j + k]);
+    vert_off.push_back(vert_off.back() + tcmp_geo_vert_off[j + 1] - v0);
+    plane_off.push_back(plane_off.back() + tcmp_geo_plane_off[j + 1] - f0);
+    edge_off.push_back(edge_off.back() + tcmp_geo_edge_off[j + 1] - tcmp_geo_edge_off[j]);
+  }
+  const int V = vert_off[n_mesh], F = plane_off[n_mesh], E = edge_off[n_mesh];
+  // device records: vertex/plane rows, Gauss-map edge records (global rows), inner boxes
+  std::vector<int> rg((size_t)std::max(n_mesh, 1) * kMrange, 0);
+  std::vector<double> ib((size_t)std::max(n_mesh, 1) * 16, 0.0);
+  std::vector<double> v64((size_t)std::max(V, 1) * 4, 0.0), p64((size_t)std::max(F, 1) * 4, 0.0),
+      e64((size_t)std::max(E, 1) * 16, 0.0);
+  for (int m = 0; m < n_mesh; ++m) {
+    int* r = rg.data() + kMrange * m;
+    r[0] = vert_off[m]; r[1] = vert_off[m + 1];
+    r[2] = plane_off[m]; r[3] = plane_off[m + 1];
+    r[4] = edge_off[m]; r[5] = edge_off[m + 1];
+    const double* b = boxes.data() + 18 * m;
+    double* d = ib.data() + 16 * m;
+    for (int k = 0; k < 12; ++k) d[k] = b[k];
+    for (int k = 0; k < 3; ++k) d[12 + k] = b[15 + k];
+  }
+  edge_records(verts.data(), vert_off.data(), planes.data(), plane_off.data(), edges.data(),
+               edge_off.data(), n_mesh, e64.data());
+  for (int v = 0; v < V; ++v)
+    for (int k = 0; k < 3; ++k) v64[4 * v + k] = verts[3 * v + k];
+  for (int f = 0; f < F; ++f)
+    for (int k = 0; k < 4; ++k) p64[4 * f + k] = planes[4 * f + k];
+  std::vector<float> v32(v64.begin(), v64.end()), p32(p64.begin(), p64.end()), e32(e64.begin(), e64.end());
+  int rc = h->mrange.ensure(rg.size());
+  rc = rc ? rc : h->mib.ensure(ib.size());
+  rc = rc ? rc : h->mv64.ensure(v64.size());
+  rc = rc ? rc : h->mp64.ensure(p64.size());
+  rc = rc ? rc : h->me64.ensure(e64.size());
+  rc = rc ? rc : h->mv32.ensure(v32.size());
+  rc = rc ? rc : h->mp32.ensure(p32.size());
+  rc = rc ? rc : h->me32.ensure(e32.size());
+  if (rc) return rc;
+  if (keep_lods)
+    for (int m = 0; m < n_user && (size_t)kMrange * (m + 1) <= h->mrange_h.size(); ++m)
+      for (int k = 6; k < kMrange; ++k) rg[kMrange * m + k] = h->mrange_h[kMrange * m + k];
+  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mp64.p, p64.data(), p64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->me64.p, e64.data(), e64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mv32.p, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mp32.p, p32.data(), p32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->mrange_h = rg;
+  return 0;
+}
+
+
 int upload_scene(tcmp_handle* h) {
   const int n = h->n_box + h->n_mesh;
-  std::vector<double> tmp((size_t)std::max(n, 1) * 16, 0.0);
+  const int n_self = h->self_coll ? TCMP_NLINKS : 0;
+  std::vector<double> tmp((size_t)std::max(n + n_self, 1) * 16, 0.0);
   std::vector<float> t32((size_t)std::max(n, 1) * 8, 0.f);
   for (int o = 0; o < h->n_box; ++o) {
     const double* s = h->box15.data() + 15 * o;
@@ -1410,6 +1492,13 @@ int upload_scene(tcmp_handle* h) {
       f[i] = (float)c;
       f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(c) + H));
     }
+  }
+  // self-collision: link j's outer box in its own frame, as the record of mesh n_mesh + j
+  for (int j = 0; j < n_self; ++j) {
+    const double* b = tcmp_geo_boxes + 18 * j;
+    double* d = tmp.data() + 16 * (n + j);
+    for (int k = 0; k < 15; ++k) d[k] = b[k];
+    d[15] = -(double)(h->n_mesh + j + 1);
   }
   if (int rc = h->obs.ensure(tmp.size())) return rc;
   if (int rc = h->obs32.ensure(t32.size())) return rc;
@@ -1482,47 +1571,8 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
     h->mesh_poff.assign(1, 0);
     h->mesh_eoff.assign(1, 0);
   }
-  // device records: vertex/plane rows, Gauss-map edge records (global rows), inner boxes
-  std::vector<int> rg((size_t)std::max(n_mesh, 1) * kMrange, 0);
-  std::vector<double> ib((size_t)std::max(n_mesh, 1) * 16, 0.0);
-  std::vector<double> v64((size_t)std::max(V, 1) * 4, 0.0), p64((size_t)std::max(F, 1) * 4, 0.0),
-      e64((size_t)std::max(E, 1) * 16, 0.0);
-  for (int m = 0; m < n_mesh; ++m) {
-    int* r = rg.data() + kMrange * m;
-    r[0] = vert_off[m]; r[1] = vert_off[m + 1];
-    r[2] = plane_off[m]; r[3] = plane_off[m + 1];
-    r[4] = edge_off[m]; r[5] = edge_off[m + 1];
-    const double* b = boxes + 18 * m;
-    double* d = ib.data() + 16 * m;
-    for (int k = 0; k < 12; ++k) d[k] = b[k];
-    for (int k = 0; k < 3; ++k) d[12 + k] = b[15 + k];
-  }
-  edge_records(verts, vert_off, planes, plane_off, edges, edge_off, n_mesh, e64.data());
-  for (int v = 0; v < V; ++v)
-    for (int k = 0; k < 3; ++k) v64[4 * v + k] = verts[3 * v + k];
-  for (int f = 0; f < F; ++f)
-    for (int k = 0; k < 4; ++k) p64[4 * f + k] = planes[4 * f + k];
-  std::vector<float> v32(v64.begin(), v64.end()), p32(p64.begin(), p64.end()), e32(e64.begin(), e64.end());
-  int rc = h->mrange.ensure(rg.size());
-  rc = rc ? rc : h->mib.ensure(ib.size());
-  rc = rc ? rc : h->mv64.ensure(v64.size());
-  rc = rc ? rc : h->mp64.ensure(p64.size());
-  rc = rc ? rc : h->me64.ensure(e64.size());
-  rc = rc ? rc : h->mv32.ensure(v32.size());
-  rc = rc ? rc : h->mp32.ensure(p32.size());
-  rc = rc ? rc : h->me32.ensure(e32.size());
-  if (rc) return rc;
-  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
-  h->mrange_h = rg;
-  HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->mp64.p, p64.data(), p64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->me64.p, e64.data(), e64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->mv32.p, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->mp32.p, p32.data(), p32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
   h->n_mesh = n_mesh;
+  if (int rc = upload_meshes(h, false)) return rc;
   return upload_scene(h);
 }
 
@@ -1563,6 +1613,15 @@ int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls
   HIPCHK(hipStreamSynchronize(h->stream));
   h->mrange_h = rg;
   return 0;
+}
+
+int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {
+  if (int rc = set_dev(h)) return rc;
+  const int on = enable ? 1 : 0;
+  if (on == h->self_coll) return 0;
+  h->self_coll = on;
+  if (int rc = upload_meshes(h, true)) return rc;
+  return upload_scene(h);
 }
 
 int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
@@ -1655,7 +1714,7 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   int rc = upload7(h, h->s0, q, n);
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
-  hipLaunchKernelGGL(h->n_mesh ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
                      (long long)n, h->scene(), h->geo(), h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
@@ -1949,7 +2008,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(h->n_mesh ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), lds_bytes(h), h->stream, P, h->st,
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), lds_bytes(h), h->stream, P, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);

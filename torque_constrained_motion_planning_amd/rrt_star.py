@@ -178,13 +178,16 @@ def _rrt_native(start, goal, distance, sample, extend, collision, torque_fn, dyn
 
 def rrt_star_batched(start, goal, obstacles, torque_mode, payload_mass, execution_time,
                      n_samples, batch=65536, seed=0, weights=None, resolutions=None,
-                     radius=0.01, goal_probability=0.2, device=0, engine=None):
-    """Engine-native batched frontier: n_samples Philox-drawn candidates, `batch` per round.
+                     radius=0.01, goal_probability=0.2, device=0, engine=None,
+                     self_collisions=False):
+    """Engine-native batched frontier: n_samples Philox-drawn candidates, `batch` per round
+    (self_collisions: the arm's self-collision pairs too, utils.py:3138-3149).
 
     Returns ((path, vels, accels, psg) | (None,)*4, PlanResult, raw arrays)."""
     from .scene import mesh_pack, obstacle_array
     eng = engine if engine is not None else _lib.engine(device)
     eng.set_scene(obstacle_array(obstacles), mesh_pack(obstacles))
+    eng.set_self_collision(self_collisions)
     st = eng.plan_begin(start, goal, torque_mode, payload_mass, execution_time,
                         max_nodes=int(n_samples) + 1, max_batch=int(batch), seed=seed,
                         weights=weights, resolutions=resolutions, radius=radius,

@@ -159,20 +159,23 @@ def get_limits_fn(body, joints, custom_limits={}, verbose=False):  # utils.py:31
 
 
 class CollisionFn:
-    """get_collision_fn (utils.py:3165-3218): joint limits, then every moving link hull vs
+    """get_collision_fn (utils.py:3165-3218): joint limits, the self-collision link pairs when
+    self_collisions (get_self_link_pairs, utils.py:3138-3149), then every moving link hull vs
     every fixed obstacle with the -MAX_DISTANCE closest-point threshold.  Evaluated by the
     engine (tcmp_check_configs)."""
 
-    def __init__(self, body, obstacles, device=0):
+    def __init__(self, body, obstacles, device=0, self_collisions=False):
         self.body = body
         self.obstacles = obstacle_array(obstacles)
         self.meshes = mesh_pack(obstacles)
         self.device = device
+        self.self_collisions = bool(self_collisions)
 
     @property
     def engine(self):
         e = _lib.engine(self.device)
         e.set_scene(self.obstacles, self.meshes)
+        e.set_self_collision(self.self_collisions)
         return e
 
     def __call__(self, q, verbose=False):
@@ -185,9 +188,9 @@ class CollisionFn:
 def get_collision_fn(body, joints, obstacles=[], attachments=[], self_collisions=True,
                      disabled_collisions=set(), custom_limits={}, use_aabb=False, cache=False,
                      max_distance=MAX_DISTANCE, **kwargs):
-    if self_collisions:
-        raise NotImplementedError("self-collision pairs are not in the engine (the reference "
-                                  "planner runs with SELF_COLLISIONS=False, utils.py:56)")
+    if disabled_collisions:
+        raise NotImplementedError("disabled_collisions are not in the engine (the reference "
+                                  "passes set(), panda_primitives.py:270)")
     if list(attachments):
         raise NotImplementedError("attachments are not in the engine (the reference planner "
                                   "passes none, panda_primitives.py:270)")
@@ -195,7 +198,7 @@ def get_collision_fn(body, joints, obstacles=[], attachments=[], self_collisions
         raise NotImplementedError("custom joint limits are not in the engine")
     if max_distance != MAX_DISTANCE:
         raise NotImplementedError("the engine's collision threshold is MAX_DISTANCE=0.04")
-    return CollisionFn(body, obstacles)
+    return CollisionFn(body, obstacles, self_collisions=self_collisions)
 
 
 def check_initial_end_force_aware(start_conf, end_conf, collision_fn, torque_fn, verbose=True):
