@@ -42,7 +42,8 @@ def test_boxes_contain_and_are_contained():
         # level-of-detail hulls: inner inside the hull, hull inside outer
         assert (inner[0] @ pl[:, :3].T <= pl[:, 3] + 1e-12).all(), name
         assert (v @ outer[1][:, :3].T <= outer[1][:, 3] + 1e-12).all(), name
-        assert len(inner[0]) <= 24 and len(inner[2]) < len(e) or len(v) <= 24
+        K = hull.INNER_LOD_K
+        assert len(inner[0]) <= K and len(inner[2]) < len(e) or len(v) <= K
         for h in (inner, outer):  # no zero-length edges (the kernels take edge vectors from
             ev = h[0][h[2][:, 1]] - h[0][h[2][:, 0]]  # fp64 differences, so short ones are fine)
             assert np.linalg.norm(ev, axis=1).min() > 1e-9, name

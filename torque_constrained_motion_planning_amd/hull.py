@@ -52,6 +52,14 @@ def hull_data(points):
     return v, np.array(planes, dtype=np.float64), np.array(edges, dtype=np.int32).reshape(-1, 4)
 
 
+# Level-of-detail sizes: the outer LOD (the "free" certificate, tested on every undecided pair)
+# takes the facet normals of a 24-vertex inner hull; the inner LOD (the "collision"
+# certificate, tested only when the outer one fails) keeps 48 vertices, so fewer colliding
+# pairs fall through to the full hull-vs-hull pass.
+INNER_LOD_K = 48
+OUTER_LOD_K = 24
+
+
 def inner_lod(verts, k=24):
     """Inner level of detail: the hull of k of the hull's vertices (a subset of the hull),
     chosen greedily -- axis extremes first, then repeatedly the vertex farthest outside the
@@ -152,8 +160,8 @@ class ConvexMesh:
             v, pl, e = hull_data(self.world_vertices())
             c, R, half, ih = fit_boxes(v, pl)
             box = np.concatenate([c, R.reshape(-1), half, ih])
-            inner = inner_lod(v)
-            outer = outer_lod(v, inner[1])
+            inner = inner_lod(v, INNER_LOD_K)
+            outer = outer_lod(v, inner_lod(v, OUTER_LOD_K)[1])
             self._rec = (v, pl, e, box, inner, outer)
         return self._rec
 
