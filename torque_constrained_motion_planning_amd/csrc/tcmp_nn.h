@@ -3,7 +3,8 @@
 // itself is k_nearest_wave32 (tcmp_nn32.h).
 //
 // Build, once per round:
-//   1. k_node_keys + radix sort: 63-bit Morton keys (9 bits per joint) of the snapshot nodes.
+//   1. k_node_keys + radix sort: Morton keys of the snapshot nodes (9 bits per joint
+//      interleaved, the top kKeyBits = 36 kept; rocPRIM Onesweep radix sort).
 //   2. k_nn_rows: stree [T][8] f64 (q0..q6, original index) and stree32 [T][8] f32 in key order.
 //   3. k_nn_cut<kNnC>: the implicit binary radix tree of the sorted keys (Karras 2012: every
 //      internal node's key range from its neighbours' common-prefix lengths) cut into
