@@ -52,12 +52,14 @@ def hull_data(points):
     return v, np.array(planes, dtype=np.float64), np.array(edges, dtype=np.int32).reshape(-1, 4)
 
 
-# Level-of-detail sizes: the outer LOD (the "free" certificate, tested on every undecided pair)
-# takes the facet normals of a 24-vertex inner hull; the inner LOD (the "collision"
-# certificate, tested only when the outer one fails) keeps 48 vertices, so fewer colliding
-# pairs fall through to the full hull-vs-hull pass.
+# Level-of-detail sizes (measured on C5, edges per 1e6 samples: outer 24 / 16 / 12 / 8 ->
+# 421 / 405 / 375 / 453 ms): the outer LOD (the "free" certificate, tested on every undecided
+# pair) takes the facet normals of a 12-vertex inner hull -- cheap, and it still certifies
+# most free pairs; the inner LOD (the "collision" certificate, tested only when the outer
+# one fails) keeps 48 vertices, so fewer colliding pairs fall through to the full
+# hull-vs-hull pass.
 INNER_LOD_K = 48
-OUTER_LOD_K = 24
+OUTER_LOD_K = 12
 
 
 def inner_lod(verts, k=24):
