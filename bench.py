@@ -203,11 +203,16 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # rehearsal of the N > 1 path on one GPU (TCMP_BENCH_BACKEND=gloo TCMP_BENCH_DEVICE=0:
+    # every rank on GPU 0, collectives over gloo on host tensors); the real run is nccl (RCCL)
+    backend = os.environ.get("TCMP_BENCH_BACKEND", "nccl")
+    gpu = int(os.environ.get("TCMP_BENCH_DEVICE", local_rank))
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         import torch
         import torch.distributed as tdist
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        torch.cuda.set_device(gpu)
+        tdist.init_process_group(backend)
         dist = tdist
 
     W = dict(WORKLOADS[args.workload])
@@ -222,7 +227,7 @@ def main():
     mode, mass = W["mode"], W["mass"]
     n_obs_total = W["boxes"] + W["meshes"]
 
-    eng = _lib.Engine(local_rank)
+    eng = _lib.Engine(gpu)
     # query ids of this rank: c4 shards 64 queries round-robin, the others run one per rank;
     # scene and goal are fixed per query id, sample seeds vary per step.  c5: one scene for all
     # ranks (query id 0), independent replica trees.
@@ -246,7 +251,7 @@ def main():
     # one 1e5-sample query's rounds do not fill the GPU on their own
     n_streams = max(1, min(len(queries), args.streams if args.streams else
                            (8 if len(queries) > 1 else 1)))
-    engines = [eng] + [_lib.Engine(local_rank) for _ in range(n_streams - 1)]
+    engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
     pool = None
     if n_streams > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -267,7 +272,7 @@ def main():
         if dist is not None:
             # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
             shard.gather_trajectories(dist, [shard.pack_trajectory(o) for o in outs],
-                                      list(qids), world, rank, device="cuda")
+                                      list(qids), world, rank, device=coll_dev)
         return res
 
     for w in range(args.warmup):
@@ -282,7 +287,7 @@ def main():
     dt = time.perf_counter() - t0
     if dist is not None:
         import torch
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt], device=coll_dev, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
 
