@@ -908,7 +908,7 @@ struct tcmp_handle {
   DBuf<int> nvals_in, svals, cvals_in, cperm;
   DBuf<double> stree, cbox;
   DBuf<float> stree32;
-  DBuf<float> cboxf, sboxf;
+  DBuf<float> cboxf, sboxf, bboxf;
   DBuf<int> chome, bcount, boff;
   DBuf<int> cflag, cid, cstart, sflag, sid, sstart;
   DBuf<unsigned long long> ckey;
@@ -1091,6 +1091,9 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0,
                      h->stream, h->st, h->sstart.p, h->cboxf.p, h->sboxf.p);
   HIPCHK(hipGetLastError());
+  hipLaunchKernelGGL(k_nn_build_blocks, dim3(grid_for(T_bound + 128, 256)), dim3(256), 0,
+                     h->stream, h->st, h->sboxf.p, h->bboxf.p);
+  HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
                      h->ckeys_in.p, h->cvals_in.p);
   HIPCHK(hipGetLastError());
@@ -1112,11 +1115,11 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   h->mark_begin(F_NNSCAN, &e0);
   if (P.uniform_w)
     hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, h->cand.p, h->cperm.p,
                        h->chome.p, nb, h->nn.p, h->second.p);
   else
     hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->cand.p, h->cperm.p,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, h->cand.p, h->cperm.p,
                        h->chome.p, nb, h->nn.p, h->second.p);
   HIPCHK(hipGetLastError());
   h->mark_end(F_NNSCAN, e0);
@@ -1302,6 +1305,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->cbox.release();
   h->cboxf.release();
   h->sboxf.release();
+  h->bboxf.release();
   h->chome.release();
   h->cflag.release();
   h->cid.release();
@@ -1885,6 +1889,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->stree32.ensure(N * 8);
   rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
   rc = rc ? rc : h->sboxf.ensure((N + 1) * 16);
+  rc = rc ? rc : h->bboxf.ensure((N / 64 + 2) * 16);
   rc = rc ? rc : h->cflag.ensure(N);
   rc = rc ? rc : h->cid.ensure(N);
   rc = rc ? rc : h->cstart.ensure(N + 1);

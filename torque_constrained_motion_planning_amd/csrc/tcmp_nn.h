@@ -163,6 +163,36 @@ __global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const int
   }
 }
 
+// blocks of 64 consecutive super-cells (Morton order): their f32 bounds, one wave per block,
+// so the scan skips a whole block of super-cell boxes with one box test
+__global__ __launch_bounds__(256) void k_nn_build_blocks(DevState* st, const float* sbox,
+                                                         float* bbox) {
+  const int nsup = st->nn_supers;
+  const long long b = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  if (b * 64 >= nsup) return;  // wave-uniform
+  const long long sp = b * 64 + lane_id();
+  float lo[7], hi[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    lo[k] = sp < nsup ? sbox[16 * sp + k] : INFINITY;
+    hi[k] = sp < nsup ? sbox[16 * sp + 8 + k] : -INFINITY;
+  }
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    lo[k] = wave_minf(lo[k]);
+    hi[k] = wave_maxf(hi[k]);
+  }
+  if (lane_id() == 0) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      bbox[16 * b + k] = lo[k];
+      bbox[16 * b + 8 + k] = hi[k];
+    }
+    bbox[16 * b + 7] = 0.f;
+    bbox[16 * b + 15] = 0.f;
+  }
+}
+
 // home cell of each Morton-sorted candidate: the cell holding its key's lower bound, and its
 // super-cell: home[j] = cell, home[nb + j] = super-cell
 __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,

@@ -63,7 +63,8 @@ template <bool UW>
 __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams P, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
-                                                        const float* sbox, const double* cand,
+                                                        const float* sbox, const float* bbox,
+                                                        const double* cand,
                                                         const int* cperm, const int* home, int nb,
                                                         int* nn, double* second) {
   const int lane = lane_id();
@@ -227,44 +228,58 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
       thr = refresh();
     }
     NN_TICK(0);
-    for (int g = 0; g < nsup; g += 64) {
-      const int sidx = zigzag(hs, g + lane, nsup);
-      int sc0 = 0, scn = 0;
-      const float lbs =
-          sidx >= 0 ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, &sc0, &scn) : INFINITY;
-      tests += (unsigned long long)min(64, nsup - g);
-      uint64_t smask = __ballot(lbs <= thr);
-      NN_TICK(1);
-      while (smask) {
-        const int i = __builtin_ctzll(smask);
-        smask &= smask - 1;
-        if (readlane_f(lbs, i) > thr) continue;
-        const int S0 = __builtin_amdgcn_readlane(sc0, i), Sn = __builtin_amdgcn_readlane(scn, i);
-        const int c = S0 + lane;
-        const bool cv = lane < Sn && c != hc;
-        int cst = 0, ccn = 0;
-        const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, &cst, &ccn) : INFINITY;
-        tests += (unsigned long long)Sn;
-        uint64_t cmask = __ballot(lbc <= thr);
-        NN_TICK(2);
-        while (cmask) {
-          int cs4[4], cn4[4];
+    // blocks of 64 super-cells, zig-zagging out from the home block (one box test each);
+    // a passing block's super-cells are tested one per lane, starting at the home super
+    const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
+    for (int gb = 0; gb < nblk; gb += 64) {
+      const int bidx = zigzag(hb, gb + lane, nblk);
+      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, s32, w32) : INFINITY;
+      tests += (unsigned long long)min(64, nblk - gb);
+      uint64_t bmask = __ballot(lbb <= thr);
+      while (bmask) {
+        const int ib = __builtin_ctzll(bmask);
+        bmask &= bmask - 1;
+        if (readlane_f(lbb, ib) > thr) continue;
+        const int blk = __builtin_amdgcn_readlane(bidx, ib);
+        const int rot = blk == hb ? (hs & 63) : 0;
+        const int sidx = 64 * blk + ((lane + rot) & 63);
+        int sc0 = 0, scn = 0;
+        const float lbs =
+            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, &sc0, &scn) : INFINITY;
+        tests += (unsigned long long)min(64, nsup - 64 * blk);
+        uint64_t smask = __ballot(lbs <= thr);
+        NN_TICK(1);
+        while (smask) {
+          const int i = __builtin_ctzll(smask);
+          smask &= smask - 1;
+          if (readlane_f(lbs, i) > thr) continue;
+          const int S0 = __builtin_amdgcn_readlane(sc0, i), Sn = __builtin_amdgcn_readlane(scn, i);
+          const int c = S0 + lane;
+          const bool cv = lane < Sn && c != hc;
+          int cst = 0, ccn = 0;
+          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, &cst, &ccn) : INFINITY;
+          tests += (unsigned long long)Sn;
+          uint64_t cmask = __ballot(lbc <= thr);
+          NN_TICK(2);
+          while (cmask) {
+            int cs4[4], cn4[4];
 #pragma unroll
-          for (int u = 0; u < 4; ++u) {
-            cs4[u] = 0;
-            cn4[u] = 0;
-            while (cmask) {
-              const int k = __builtin_ctzll(cmask);
-              cmask &= cmask - 1;
-              if (readlane_f(lbc, k) <= thr) {
-                cs4[u] = __builtin_amdgcn_readlane(cst, k);
-                cn4[u] = __builtin_amdgcn_readlane(ccn, k);
-                break;
+            for (int u = 0; u < 4; ++u) {
+              cs4[u] = 0;
+              cn4[u] = 0;
+              while (cmask) {
+                const int k = __builtin_ctzll(cmask);
+                cmask &= cmask - 1;
+                if (readlane_f(lbc, k) <= thr) {
+                  cs4[u] = __builtin_amdgcn_readlane(cst, k);
+                  cn4[u] = __builtin_amdgcn_readlane(ccn, k);
+                  break;
+                }
               }
             }
+            if (cn4[0] > 0) thr = scan4(cs4, cn4);
+            NN_TICK(3);
           }
-          if (cn4[0] > 0) thr = scan4(cs4, cn4);
-          NN_TICK(3);
         }
       }
     }
