@@ -194,6 +194,8 @@ def main():
                     help="host cores for the multi-core CPU baseline (16 = one GPU's share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--self-collisions", action="store_true",
+                    help="add the arm's self-collision pairs (off in the reference planner)")
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 8 for c4)")
@@ -235,6 +237,7 @@ def main():
         qids = shard.queries_for_rank(W["queries"], world, rank)
     else:
         qids = [0 if args.workload == "c5" else rank]
+    eng.set_self_collision(args.self_collisions)
     queries = [make_query(1234 + q, n_obs=W["boxes"], mode=mode, mass=mass, engine=eng,
                           n_mesh=W["meshes"]) for q in qids]
 
@@ -252,6 +255,8 @@ def main():
     n_streams = max(1, min(len(queries), args.streams if args.streams else
                            (8 if len(queries) > 1 else 1)))
     engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
+    for e in engines[1:]:
+        e.set_self_collision(args.self_collisions)
     pool = None
     if n_streams > 1:
         from concurrent.futures import ThreadPoolExecutor
@@ -355,7 +360,8 @@ def main():
         "config": {"workload": W["text"], "boxes": W["boxes"], "meshes": W["meshes"],
                    "samples_per_query": W["samples"], "queries_per_step": n_queries_total,
                    "batch_per_round": W["batch"], "execution_time_s": 5.0,
-                   "parallelism": "query-sharded x%d" % world, "streams_per_gpu": n_streams},
+                   "parallelism": "query-sharded x%d" % world, "streams_per_gpu": n_streams,
+                   "self_collisions": bool(args.self_collisions)},
         "roofline": dominant,
         "roofline_other": other,
         "hbm_roofline": {"bytes_per_step": hbm_bytes / S, "achieved": hbm_gbs, "unit": "GB/s",
