@@ -888,6 +888,10 @@ struct tcmp_handle {
   DBuf<double> mib, mv64, mp64, me64;
   DBuf<float> mv32, mp32, me32;
   DBuf<float> lv32[2], lp32[2], le32[2];      // mesh LOD hulls (inner, outer), world frame
+  // host copies of the user meshes' LOD hulls (tcmp_set_mesh_lods; cleared by tcmp_set_meshes)
+  bool user_lods = false;
+  std::vector<double> lod_v[2], lod_p[2];
+  std::vector<int> lod_e[2], lod_vo[2], lod_po[2], lod_eo[2];
   DBuf<float> lodv3[2], lodpl[2];             // link LOD hulls (panda_lod.inc), link frames
   DBuf<unsigned short> lodei[2];
   DBuf<float> lodev[2], geo_ev;               // link hull edge vectors (fp64 -> fp32)
@@ -1380,10 +1384,11 @@ int check_hulls(const tcmp_hulls* H, int n, const char* what) {
   return 0;
 }
 
+int upload_lods(tcmp_handle* h);
+
 // Device mesh arrays from the host copies: the user meshes, then (self-collision on) the 10
-// link hulls in their own link frames as meshes n_mesh + j.  keep_lods: the user meshes'
-// level-of-detail rows (tcmp_set_mesh_lods) survive the rebuild.
-int upload_meshes(tcmp_handle* h, bool keep_lods) {
+// link hulls in their own link frames as meshes n_mesh + j; then their LOD rows.
+int upload_meshes(tcmp_handle* h) {
   const int n_user = h->n_mesh, n_self = h->self_coll ? TCMP_NLINKS : 0;
   const int n_mesh = n_user + n_self;
   std::vector<double> verts(h->mesh_v), planes(h->mesh_p), boxes(h->mesh_box);
@@ -1440,9 +1445,6 @@ int upload_meshes(tcmp_handle* h, bool keep_lods) {
   rc = rc ? rc : h->mp32.ensure(p32.size());
   rc = rc ? rc : h->me32.ensure(e32.size());
   if (rc) return rc;
-  if (keep_lods)
-    for (int m = 0; m < n_user && (size_t)kMrange * (m + 1) <= h->mrange_h.size(); ++m)
-      for (int k = 6; k < kMrange; ++k) rg[kMrange * m + k] = h->mrange_h[kMrange * m + k];
   HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -1451,6 +1453,70 @@ int upload_meshes(tcmp_handle* h, bool keep_lods) {
   HIPCHK(hipMemcpyAsync(h->mv32.p, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mp32.p, p32.data(), p32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->mrange_h = rg;
+  return upload_lods(h);
+}
+
+// Level-of-detail hulls of the meshes (rows 6..17 of mrange, flag 18): the user meshes'
+// (tcmp_set_mesh_lods, world frame) followed, self-collision on, by the links' own LODs
+// (panda_lod.inc, link frames) for the link meshes n_mesh + j.
+int upload_lods(tcmp_handle* h) {
+  const int n_user = h->user_lods ? h->n_mesh : 0, n_self = h->self_coll ? TCMP_NLINKS : 0;
+  if (n_user + n_self == 0) return 0;
+  std::vector<int> rg = h->mrange_h;
+  const double* lv[2] = {tcmp_lod_in_verts, tcmp_lod_out_verts};
+  const double* lp[2] = {tcmp_lod_in_planes, tcmp_lod_out_planes};
+  const unsigned short* le[2] = {tcmp_lod_in_edges, tcmp_lod_out_edges};
+  const int* lvo[2] = {tcmp_lod_in_vert_off, tcmp_lod_out_vert_off};
+  const int* lpo[2] = {tcmp_lod_in_plane_off, tcmp_lod_out_plane_off};
+  const int* leo[2] = {tcmp_lod_in_edge_off, tcmp_lod_out_edge_off};
+  for (int i = 0; i < 2; ++i) {
+    std::vector<double> v, pl;
+    std::vector<int> e, vo{0}, po{0}, eo{0};
+    if (n_user) {
+      v = h->lod_v[i]; pl = h->lod_p[i]; e = h->lod_e[i];
+      vo = h->lod_vo[i]; po = h->lod_po[i]; eo = h->lod_eo[i];
+    }
+    for (int j = 0; j < n_self; ++j) {
+      for (int r = lvo[i][j]; r < lvo[i][j + 1]; ++r)
+        for (int k = 0; k < 3; ++k) v.push_back(lv[i][3 * r + k]);
+      for (int r = lpo[i][j]; r < lpo[i][j + 1]; ++r)
+        for (int k = 0; k < 4; ++k) pl.push_back(lp[i][4 * r + k]);
+      for (int r = leo[i][j]; r < leo[i][j + 1]; ++r) {
+        const unsigned short* q = le[i] + 4 * r;
+        e.push_back(q[0] - lvo[i][j]); e.push_back(q[1] - lvo[i][j]);
+        e.push_back(q[2] - lpo[i][j]); e.push_back(q[3] - lpo[i][j]);
+      }
+      vo.push_back(vo.back() + lvo[i][j + 1] - lvo[i][j]);
+      po.push_back(po.back() + lpo[i][j + 1] - lpo[i][j]);
+      eo.push_back(eo.back() + leo[i][j + 1] - leo[i][j]);
+    }
+    const int nm = n_user + n_self, V = vo[nm], F = po[nm], E = eo[nm];
+    std::vector<double> e64((size_t)E * 16);
+    edge_records(v.data(), vo.data(), pl.data(), po.data(), e.data(), eo.data(), nm, e64.data());
+    std::vector<float> v32((size_t)V * 4, 0.f), p32(pl.begin(), pl.end()), e32(e64.begin(), e64.end());
+    for (int r = 0; r < V; ++r)
+      for (int k = 0; k < 3; ++k) v32[4 * r + k] = (float)v[3 * r + k];
+    int rc = h->lv32[i].ensure(v32.size());
+    rc = rc ? rc : h->lp32[i].ensure(p32.size());
+    rc = rc ? rc : h->le32[i].ensure(e32.size());
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h->lv32[i].p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->lp32[i].p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipMemcpyAsync(h->le32[i].p, e32.data(), e32.size() * 4, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
+    for (int m = 0; m < nm; ++m) {
+      // LOD hull m belongs to mesh m (user) or to link mesh h->n_mesh + (m - n_user)
+      const int mesh = m < n_user ? m : h->n_mesh + (m - n_user);
+      int* r = rg.data() + kMrange * mesh + 6 + 6 * i;
+      r[0] = vo[m]; r[1] = vo[m + 1];
+      r[2] = po[m]; r[3] = po[m + 1];
+      r[4] = eo[m]; r[5] = eo[m + 1];
+      rg[kMrange * mesh + 18] = 1;
+    }
+  }
+  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->mrange_h = rg;
   return 0;
@@ -1576,7 +1642,8 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
     h->mesh_eoff.assign(1, 0);
   }
   h->n_mesh = n_mesh;
-  if (int rc = upload_meshes(h, false)) return rc;
+  h->user_lods = false;  // new meshes: their LODs come with the next tcmp_set_mesh_lods
+  if (int rc = upload_meshes(h)) return rc;
   return upload_scene(h);
 }
 
@@ -1588,35 +1655,17 @@ int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls
   if (int rc = check_hulls(inner, n_mesh, "inner")) return rc;
   if (int rc = check_hulls(outer, n_mesh, "outer")) return rc;
   const tcmp_hulls* H[2] = {inner, outer};
-  std::vector<int> rg = h->mrange_h;
   for (int i = 0; i < 2; ++i) {
     const int V = H[i]->vert_off[n_mesh], F = H[i]->plane_off[n_mesh], E = H[i]->edge_off[n_mesh];
-    std::vector<double> e64((size_t)E * 16);
-    edge_records(H[i]->verts, H[i]->vert_off, H[i]->planes, H[i]->plane_off, H[i]->edges,
-                 H[i]->edge_off, n_mesh, e64.data());
-    std::vector<float> v32((size_t)V * 4, 0.f), p32(H[i]->planes, H[i]->planes + 4 * (size_t)F),
-        e32(e64.begin(), e64.end());
-    for (int v = 0; v < V; ++v)
-      for (int k = 0; k < 3; ++k) v32[4 * v + k] = (float)H[i]->verts[3 * v + k];
-    int rc = h->lv32[i].ensure(v32.size());
-    rc = rc ? rc : h->lp32[i].ensure(p32.size());
-    rc = rc ? rc : h->le32[i].ensure(e32.size());
-    if (rc) return rc;
-    HIPCHK(hipMemcpyAsync(h->lv32[i].p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(h->lp32[i].p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipMemcpyAsync(h->le32[i].p, e32.data(), e32.size() * 4, hipMemcpyHostToDevice, h->stream));
-    for (int m = 0; m < n_mesh; ++m) {
-      int* r = rg.data() + kMrange * m + 6 + 6 * i;
-      r[0] = H[i]->vert_off[m]; r[1] = H[i]->vert_off[m + 1];
-      r[2] = H[i]->plane_off[m]; r[3] = H[i]->plane_off[m + 1];
-      r[4] = H[i]->edge_off[m]; r[5] = H[i]->edge_off[m + 1];
-    }
+    h->lod_v[i].assign(H[i]->verts, H[i]->verts + 3 * (size_t)V);
+    h->lod_p[i].assign(H[i]->planes, H[i]->planes + 4 * (size_t)F);
+    h->lod_e[i].assign(H[i]->edges, H[i]->edges + 4 * (size_t)E);
+    h->lod_vo[i].assign(H[i]->vert_off, H[i]->vert_off + n_mesh + 1);
+    h->lod_po[i].assign(H[i]->plane_off, H[i]->plane_off + n_mesh + 1);
+    h->lod_eo[i].assign(H[i]->edge_off, H[i]->edge_off + n_mesh + 1);
   }
-  for (int m = 0; m < n_mesh; ++m) rg[kMrange * m + 18] = 1;
-  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  h->mrange_h = rg;
-  return 0;
+  h->user_lods = true;
+  return upload_lods(h);
 }
 
 int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {
@@ -1624,7 +1673,7 @@ int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {
   const int on = enable ? 1 : 0;
   if (on == h->self_coll) return 0;
   h->self_coll = on;
-  if (int rc = upload_meshes(h, true)) return rc;
+  if (int rc = upload_meshes(h)) return rc;
   return upload_scene(h);
 }
 
