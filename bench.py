@@ -56,9 +56,11 @@ def pmc_traffic(kernel):
 
 
 # BASELINE.json configs (SURVEY 8 sizes): boxes, meshes, torque test, payload, samples per
-# query, queries per step (all ranks together), scaling
+# query, queries per step (all ranks together), scaling.  Batch per round: SURVEY 8d's
+# 65,536 for the 1e5-sample queries (C2 17.4M -> 28.0M, C4 26.7M -> 39.7M samples/s over
+# 32,768), 262,144 for the 1e6 / 1e7-sample ones.
 WORKLOADS = {
-    "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=32768,
+    "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=65536,
                queries=1, scaling="weak",
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step"),
@@ -66,7 +68,7 @@ WORKLOADS = {
                batch=262144, queries=1, scaling="weak",
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
-    "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=32768,
+    "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
                queries=64, scaling="strong",
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
                     "samples each) per step, sharded round-robin over the GPUs, solved paths "
