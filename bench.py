@@ -200,7 +200,7 @@ def main():
                     help="add the arm's self-collision pairs (off in the reference planner)")
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
-                         "when a rank plans several queries per step (default 8 for c4)")
+                         "when a rank plans several queries per step (default 16 for c4, at most one per query)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -255,7 +255,7 @@ def main():
     # (handles, one HIP stream each) from host threads -- the C-ABI calls release the GIL and
     # one 1e5-sample query's rounds do not fill the GPU on their own
     n_streams = max(1, min(len(queries), args.streams if args.streams else
-                           (8 if len(queries) > 1 else 1)))
+                           (16 if len(queries) > 1 else 1)))
     engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
     for e in engines[1:]:
         e.set_self_collision(args.self_collisions)
