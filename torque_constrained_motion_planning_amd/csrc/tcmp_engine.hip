@@ -325,6 +325,7 @@ struct EdgeJob {
   int* nsafe;
   int* nsteps;
   double* last;             // stride 8
+  const int* order;         // nullable: the k-th edge taken is order[k] (longest first)
 };
 
 #ifndef TCMP_EDGE_MINW
@@ -366,7 +367,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
       if (need) {
         const int my = base + (int)__popcll(m & ((1ull << lane) - 1ull));
         if (my < J.n) {
-          e = my;
+          e = J.order ? J.order[my] : my;
           const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
           load7(J.from_base + 8 * src, q);
           load7(J.to + 8 * (size_t)e, q2);
@@ -1130,6 +1131,22 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   return 0;
 }
 
+// planned step count of each round edge (nearest node -> candidate) as an ascending sort key
+// for longest-first scheduling of k_edges
+constexpr int kEdgeOrderMin = 4096;
+__global__ void k_edge_order_keys(PlanParams P, const double* cfg, const int* nn,
+                                  const double* cand, int nb, unsigned long long* keys,
+                                  int* vals) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nb) return;
+  double a[7], b[7];
+  load7(cfg + 8 * (size_t)nn[e], a);
+  load7(cand + 8 * (size_t)e, b);
+  const int n = num_steps(a, b, P.res);
+  keys[e] = (unsigned long long)(255 - min(n, 255));
+  vals[e] = e;
+}
+
 int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
   if (J.n <= 0) return 0;
   HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
@@ -1795,7 +1812,7 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
     for (int k = 0; k < 7; ++k) P.res[k] = resolutions[k];
   P.torque_mode = torque_mode;
   P.mass = payload_mass;
-  EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p};
+  EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p, nullptr};
   if ((rc = launch_edges(h, J, P))) return rc;
   std::vector<double> tmp((size_t)n * 8);
   HIPCHK(hipMemcpyAsync(n_safe, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -2039,7 +2056,19 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   h->mark_end(F_NEAREST, e0);
   h->launches_nearest++;
   h->mark_begin(F_EDGES, &e0);
-  EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p};
+  EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p, nullptr};
+  if (nb >= kEdgeOrderMin) {
+    // longest planned edges first (the persistent lanes then finish together): 8-bit keys
+    // 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
+    hipLaunchKernelGGL(k_edge_order_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P,
+                       h->cfg.p, h->nn.p, h->cand.p, nb, h->ckeys_in.p, h->cvals_in.p);
+    HIPCHK(hipGetLastError());
+    size_t tb = h->sort_tmp.n;
+    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
+                                               h->cvals_in.p, h->cperm.p, (size_t)nb, 0, 8,
+                                               h->stream));
+    J.order = h->cperm.p;
+  }
   if (int rc = launch_edges(h, J, P)) return rc;
   h->mark_end(F_EDGES, e0);
   h->mark_begin(F_INSERT, &e0);
