@@ -232,13 +232,16 @@ def main():
     n_obs_total = W["boxes"] + W["meshes"]
 
     eng = _lib.Engine(gpu)
-    # query ids of this rank: c4 shards 64 queries round-robin, the others run one per rank;
-    # scene and goal are fixed per query id, sample seeds vary per step.  c5: one scene for all
-    # ranks (query id 0), independent replica trees.
+    # query ids of this rank: c4 shards 64 queries round-robin (scene and goal fixed per query
+    # id); the single-query workloads run the same scene (query id 0) on every rank with
+    # rank-dependent sample seeds -- independent trees of identical expected work, so the
+    # per-GPU work stays fixed as N grows (weak scaling; c5 splits its samples instead)
     if W["queries"] > 1:
         qids = shard.queries_for_rank(W["queries"], world, rank)
+        labels = list(qids)
     else:
-        qids = [0 if args.workload == "c5" else rank]
+        qids = [0]
+        labels = [rank]
     eng.set_self_collision(args.self_collisions)
     queries = [make_query(1234 + q, n_obs=W["boxes"], mode=mode, mass=mass, engine=eng,
                           n_mesh=W["meshes"]) for q in qids]
@@ -279,7 +282,7 @@ def main():
         if dist is not None:
             # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
             shard.gather_trajectories(dist, [shard.pack_trajectory(o) for o in outs],
-                                      list(qids), world, rank, device=coll_dev)
+                                      labels, world, rank, device=coll_dev)
         return res
 
     for w in range(args.warmup):
