@@ -117,7 +117,9 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
                      int32_t* n_safe, int32_t* n_steps, double* last);
 
 /* argmin over tree nodes of the weighted distance (rrt_star.py:9-14,171), first index wins
- * ties.  tree: T x 7, samples: n x 7, weights: 7 (NULL = 10 = 1/radius). */
+ * ties.  tree: T x 7, samples: n x 7, weights: 7 positive (NULL = 10 = 1/radius).  Runs the
+ * planner's own nearest path: the radix-tree cell index of the tree and the pruned exact
+ * scan k_nearest_wave32 (fp32 first pass, fp64 decision). */
 int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* samples,
                  int64_t n, const double* weights, int32_t* idx);
 
@@ -212,6 +214,14 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
 /* debug: tree snapshot (cfg n x 7, cost n, parent n). */
 int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32_t* parent,
                    int64_t* n);
+
+/* debug: the last round's nearest-neighbour step (rrt_star.py:171 for every lane): its nb
+ * candidates (cand nb x 7), the chosen nearest node of each (nn, an index into the tree) and
+ * the exact fp64 score of that node (sum_k (s_k - n_k)^2 when the weights are uniform, else
+ * sum_k w_k (s_k - n_k)^2); snap = the snapshot size the round searched (nodes [0, snap)).
+ * The first min(cap, nb) rows are copied; any array pointer may be NULL. */
+int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn,
+                          double* score, int64_t* snap, int32_t* nb);
 
 #ifdef __cplusplus
 }

@@ -68,6 +68,7 @@ def lib():
         L.orc_self_pairs.argtypes = [_ip]
         L.orc_self_pair_pd.argtypes = [ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int]
         L.orc_self_pair_pd.restype = ctypes.c_double
+        L.orc_nearest.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_long, _dp, _ip, _dp]
         L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
                                   ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
         assert L.orc_sizeof_cfg() == ctypes.sizeof(RrtCfg), "oracle cfg layout mismatch"
@@ -230,6 +231,15 @@ def ik8(T, q7):
     lib().orc_ik8(_d(R), _d(p), float(q7), _d(sols), valid.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
     idx = np.nonzero(valid)[0]
     return sols.reshape(8, 7)[idx], idx
+
+
+def nearest(tree, samples, weights=None):
+    """argmin over tree rows of the weighted distance (rrt_star.py:9-14): (idx, dist)."""
+    t = _arr(tree, (-1, 7)); s = _arr(samples, (-1, 7))
+    w = _arr(np.full(7, 10.0) if weights is None else weights, (7,))
+    idx = np.zeros(len(s), dtype=np.int32); dist = np.zeros(len(s))
+    lib().orc_nearest(_d(t), len(t), _d(s), len(s), _d(w), idx.ctypes.data_as(_ip), _d(dist))
+    return idx, dist
 
 
 def philox_uniforms(seed, k):

@@ -1279,5 +1279,22 @@ done:
   return res->status;
 }
 
+/* argmin (rrt_star.py:9-14) of distance(node, s) over nodes [0, T) for each of n samples
+ * (rrt_star.py:171): a linear scan, strict < so the first index wins ties.  idx[j], and
+ * dist[j] = the winning weighted distance (get_distance_fn, utils.py:3010-3017). */
+ORC_API void orc_nearest(const double* tree, long T, const double* S, long n, const double* w,
+                         int* idx, double* dist) {
+  for (long j = 0; j < n; ++j) {
+    double best = INFINITY;
+    long bi = 0;
+    for (long t = 0; t < T; ++t) {
+      const double d = orc_dist(tree + 7 * t, S + 7 * j, w);
+      if (d < best) { best = d; bi = t; }
+    }
+    idx[j] = (int)bi;
+    dist[j] = best;
+  }
+}
+
 ORC_API int orc_sizeof_cfg(void) { return (int)sizeof(orc_rrt_cfg); }
 ORC_API int orc_sizeof_result(void) { return (int)sizeof(orc_rrt_result); }

@@ -108,15 +108,39 @@ def test_check_edges_vs_oracle(eng):
 
 
 def test_nearest_exact(eng):
+    """tcmp_nearest runs the planner's own index + k_nearest_wave32 (rrt_star.py:9-14)."""
     rng = np.random.default_rng(3)
     tree = rand_q(rng, 5000)
     tree[100] = tree[7]  # duplicate: first index must win
     s = rand_q(rng, 1000)
     s[0] = tree[7]
     idx = eng.nearest(tree, s)
-    d = ((s[:, None, :] - tree[None, :, :]) ** 2).sum(-1)
-    assert (idx == d.argmin(1)).all()
+    ref, _ = O.nearest(tree, s)
+    assert (idx == ref).all()
     assert idx[0] == 7
+    # many exact duplicates (cells of identical keys), a single-node tree
+    dup = np.repeat(rand_q(rng, 50), 40, axis=0)
+    s2 = np.concatenate([dup[::97], rand_q(rng, 300)])
+    assert (eng.nearest(dup, s2) == O.nearest(dup, s2)[0]).all()
+    assert (eng.nearest(tree[:1], s) == 0).all()
+
+
+def test_nearest_weights_and_range(eng):
+    """Non-uniform weights (the weighted scan) and coordinates outside the joint-limit box
+    (the fp32 error terms scale with the data's bound)."""
+    rng = np.random.default_rng(4)
+    tree = rand_q(rng, 40000)
+    s = rand_q(rng, 3000)
+    w = np.array([10.0, 3.0, 7.5, 1.0, 20.0, 0.5, 10.0])
+    assert (eng.nearest(tree, s, w) == O.nearest(tree, s, w)[0]).all()
+    big = rng.uniform(-40, 40, (20000, 7))
+    sb = rng.uniform(-40, 40, (2000, 7))
+    assert (eng.nearest(big, sb) == O.nearest(big, sb)[0]).all()
+    # clustered nodes (a grown tree is dense near its edges): near-ties within fp32 resolution
+    base = rand_q(rng, 1)
+    clus = base + rng.normal(0, 1e-5, (30000, 7))
+    sc = base + rng.normal(0, 2e-5, (2000, 7))
+    assert (eng.nearest(clus, sc) == O.nearest(clus, sc)[0]).all()
 
 
 def test_validate_traj_vs_oracle(eng):

@@ -26,7 +26,8 @@ EXPORTS = [
     "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
-    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_ik", "tcmp_fk", "tcmp_debug_counters",
+    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
+    "tcmp_debug_counters",
 ]
 
 
@@ -111,6 +112,7 @@ def load_library(path=LIB_PATH):
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
+        L.tcmp_plan_debug_round.argtypes = [vp, ctypes.c_int64, _dp, _i32p, _dp, _i64p, _i32p]
         L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
         L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
         L.tcmp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
@@ -356,6 +358,16 @@ class Engine:
                                           par.ctypes.data_as(_i32p), ctypes.byref(n)))
         m = min(cap, n.value)
         return cfg[:m], cost[:m], par[:m], n.value
+
+    def plan_debug_round(self, cap):
+        """The last round's (candidates, nearest index, exact score, snapshot size)."""
+        cand = np.zeros((cap, 7)); nn = np.zeros(cap, dtype=np.int32); score = np.zeros(cap)
+        snap = ctypes.c_int64(0); nb = ctypes.c_int32(0)
+        self._check(self.L.tcmp_plan_debug_round(self.h, int(cap), _d(cand),
+                                                 nn.ctypes.data_as(_i32p), _d(score),
+                                                 ctypes.byref(snap), ctypes.byref(nb)))
+        m = min(cap, nb.value)
+        return cand[:m], nn[:m], score[:m], snap.value
 
 
 _engines = {}

@@ -8,8 +8,8 @@
 // Round structure (batched frontier, B candidates per round, one HIP stream):
 //   k_sample        Philox4x32-10 candidate draws (or host-provided draws)
 //   nearest         per-round radix-tree cell index of the snapshot (tcmp_nn.h) and the
-//                   pruned exact scan k_nearest_wave32 (tcmp_nn32.h); k_nearest below is
-//                   the brute-force scan behind tcmp_nearest and TCMP_NN_BRUTE=1
+//                   pruned exact scan k_nearest_wave32 (tcmp_nn32.h); tcmp_nearest runs
+//                   the same index and scan over a caller's tree
 //   k_edges         persistent lane-refill edge walker: extend steps, collision, torque
 //   k_ins_*         lane-ordered insertion (device-wide scan), goal test (tcmp_insert.h)
 //   k_rewire_scan   neighbours within radius of each new node (snapshot)
@@ -21,6 +21,7 @@
 
 #include <algorithm>
 #include <climits>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -49,9 +50,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 constexpr int kNbrCap = 8;     // stored rewire neighbours per flagged new node
-constexpr int kMaxSplits = 64; // tree splits of k_nearest
-constexpr int kNnTile = 256;   // tree nodes per LDS tile
-constexpr int kNnCpt = 2;      // candidates per thread in k_nearest
+constexpr int kNnTile = 256;   // snapshot nodes per LDS tile of k_rewire_scan
 
 struct DevState {
   long long n_nodes;
@@ -81,6 +80,7 @@ struct DevState {
 struct PlanParams {
   double start[7], goal[7], w[7], res[7];
   double radius, goal_prob, goal_tol, mass, exec_time;
+  double nn_cmax;  // bound on |q| of nodes and candidates (fp32 error terms of tcmp_nn32.h)
   unsigned long long seed;
   int torque_mode;
   int uniform_w;
@@ -143,93 +143,6 @@ __global__ void k_goal_fix(PlanParams P, DevState* st, double* cand, unsigned ch
 }
 
 // ------------------------------------------------------------------------------------------
-// k_nearest: argmin_n sum_k w_k (s_k - n_k)^2 over the snapshot, ties -> lowest index
-// (rrt_star.py:9-14,171).  grid = (candidate blocks, tree splits): block (x, y) scores
-// 256 x kNnCpt candidates against nodes [y*split_len, (y+1)*split_len); the nodes stream
-// through LDS in 256-node tiles (16 KiB) read by broadcast.  Each candidate also tracks its
-// second-smallest distance: k_nn_merge uses it to prove that no node other than the nearest
-// can lie within the rewire radius of the new node (triangle inequality), so the full
-// neighbour scan of rrt_star.py:183 runs only for the rare lanes where that proof fails.
-// ------------------------------------------------------------------------------------------
-template <bool UW>
-__global__ __launch_bounds__(256) void k_nearest(PlanParams P, DevState* st, const double* tree,
-                                                 long long T_override, const double* cand,
-                                                 int nb, long long split_len, double* pd1,
-                                                 int* pidx, double* pd2) {
-  __shared__ double4 tile[2 * kNnTile];
-  const int tid = threadIdx.x;
-  const long long T = T_override >= 0 ? T_override : st->n_nodes;
-  const long long lo = (long long)blockIdx.y * split_len;
-  const long long hi = min(T, lo + split_len);
-  double s[kNnCpt][7];
-  double b1[kNnCpt], b2[kNnCpt];
-  int bi[kNnCpt];
-#pragma unroll
-  for (int c = 0; c < kNnCpt; ++c) {
-    const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
-    b1[c] = INFINITY;
-    b2[c] = INFINITY;
-    bi[c] = INT_MAX;
-    if (j < nb) {
-      load7(cand + 8 * (size_t)j, s[c]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 7; ++k) s[c][k] = 0;
-    }
-  }
-  double w[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) w[k] = P.w[k];
-  const double4* t4 = reinterpret_cast<const double4*>(tree);
-  for (long long base = lo; base < hi; base += kNnTile) {
-    const long long n = base + tid;
-    if (n < hi) {
-      tile[2 * tid] = t4[2 * n];
-      tile[2 * tid + 1] = t4[2 * n + 1];
-    }
-    __syncthreads();
-    const int cnt = (int)min((long long)kNnTile, hi - base);
-    for (int jj = 0; jj < cnt; ++jj) {
-      const double4 a = tile[2 * jj], b = tile[2 * jj + 1];
-#pragma unroll
-      for (int c = 0; c < kNnCpt; ++c) {
-        const double d0 = s[c][0] - a.x, d1 = s[c][1] - a.y, d2 = s[c][2] - a.z,
-                     d3 = s[c][3] - a.w, d4 = s[c][4] - b.x, d5 = s[c][5] - b.y,
-                     d6 = s[c][6] - b.z;
-        double dd;
-        if (UW) {
-          dd = d0 * d0;
-          dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
-          dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
-        } else {
-          dd = w[0] * (d0 * d0);
-          dd = fma(w[1] * d1, d1, dd); dd = fma(w[2] * d2, d2, dd); dd = fma(w[3] * d3, d3, dd);
-          dd = fma(w[4] * d4, d4, dd); dd = fma(w[5] * d5, d5, dd); dd = fma(w[6] * d6, d6, dd);
-        }
-        // top-2 (strict <: the first index keeps ties, rrt_star.py:14)
-        const bool lt1 = dd < b1[c];
-        b2[c] = lt1 ? b1[c] : fmin(b2[c], dd);
-        b1[c] = lt1 ? dd : b1[c];
-        bi[c] = lt1 ? (int)(base + jj) : bi[c];
-      }
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int c = 0; c < kNnCpt; ++c) {
-    const int j = blockIdx.x * (256 * kNnCpt) + tid + 256 * c;
-    if (j < nb) {
-      const size_t o = (size_t)blockIdx.y * nb + j;
-      pd1[o] = b1[c];
-      pidx[o] = bi[c];
-      pd2[o] = b2[c];
-    }
-  }
-  if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0)
-    atomicAdd(&st->nn_pairs, (unsigned long long)nb * (unsigned long long)T);
-}
-
-// ------------------------------------------------------------------------------------------
 // Morton keys of snapshot nodes and candidates for the nearest-neighbour index (tcmp_nn.h):
 // 9 bits per joint over the joint limits, interleaved, and only the top kKeyBits kept --
 // 2^36 cells leave at most a handful of nodes per cell, and the radix sorts run 5 digit
@@ -286,30 +199,6 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
 #include "tcmp_nn32.h"
 #include "tcmp_insert.h"
 #include "tcmp_ik.h"
-
-// merge the per-split partial results: nearest index and the second-smallest distance
-template <bool UW>
-__global__ void k_nn_merge(int nb, int splits, const double* pd1, const int* pidx,
-                           const double* pd2, int* nn, double* second) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= nb) return;
-  double b1 = INFINITY, b2 = INFINITY;
-  int bi = INT_MAX;
-  for (int y = 0; y < splits; ++y) {
-    const size_t o = (size_t)y * nb + j;
-    const double d1 = pd1[o], d2 = pd2[o];
-    const int i1 = pidx[o];
-    if (d1 < b1 || (d1 == b1 && i1 < bi)) {
-      b2 = fmin(b1, d2);
-      b1 = d1;
-      bi = i1;
-    } else {
-      b2 = fmin(b2, d1);
-    }
-  }
-  nn[j] = bi == INT_MAX ? 0 : bi;
-  if (second) second[j] = b2;
-}
 
 // ------------------------------------------------------------------------------------------
 // k_edges: safe_path_force_aware(extend(from, to)) for n edges (rrt_star.py:90-98).
@@ -906,8 +795,9 @@ struct tcmp_handle {
   DBuf<int2> meta;
   DBuf<double> cand, last;
   DBuf<unsigned char> cgoal;
-  DBuf<int> nn, nsafe, nsteps, nbr, ncount, pidx, rwlist;
-  DBuf<double> pd1, pd2;
+  DBuf<int> nn, nsafe, nsteps, nbr, ncount, rwlist;
+  DBuf<double> nnscore;  // the last round's best exact score per candidate (tcmp_plan_debug_round)
+  int last_nb = 0;
   // Morton-chunked snapshot
   DBuf<unsigned long long> nkeys_in, skeys, ckeys_in, ckeys;
   DBuf<int> nvals_in, svals, cvals_in, cperm;
@@ -918,7 +808,7 @@ struct tcmp_handle {
   DBuf<int> cflag, cid, cstart, sflag, sid, sstart;
   DBuf<unsigned long long> ckey;
   DBuf<unsigned char> sort_tmp;
-  bool nn_brute = false;
+  DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
   int nn_waves_per_cu = 16;
   DBuf<double> second;
   DBuf<long long> chain;
@@ -1026,80 +916,94 @@ unsigned lds_bytes(const tcmp_handle* h) {
 
 unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>(1, (n + block - 1) / block); }
 
-// k_nearest over a tree of at most T_bound nodes (T_exact >= 0: known size), then merge.
-int launch_nearest(tcmp_handle* h, const PlanParams& P, const double* tree, long long T_bound,
-                   long long T_exact, const double* cand, int nb, int* nn, double* second) {
-  const int cblocks = (nb + 256 * kNnCpt - 1) / (256 * kNnCpt);
-  const long long want = std::max<long long>(1, (8LL * h->cu_count + cblocks - 1) / cblocks);
-  long long splits = std::min<long long>(want, std::max<long long>(1, T_bound / 2048));
-  splits = std::min<long long>(splits, kMaxSplits);
-  long long len = (T_bound + splits - 1) / splits;
-  len = ((len + kNnTile - 1) / kNnTile) * kNnTile;
-  splits = std::max<long long>(1, (T_bound + len - 1) / len);
-  if (int rc = h->pd1.ensure((size_t)splits * nb)) return rc;
-  if (int rc = h->pd2.ensure((size_t)splits * nb)) return rc;
-  if (int rc = h->pidx.ensure((size_t)splits * nb)) return rc;
-  const dim3 grid((unsigned)cblocks, (unsigned)splits);
-  if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest<true>, grid, dim3(256), 0, h->stream, P, h->st, tree, T_exact,
-                       cand, nb, len, h->pd1.p, h->pidx.p, h->pd2.p);
-  else
-    hipLaunchKernelGGL(k_nearest<false>, grid, dim3(256), 0, h->stream, P, h->st, tree, T_exact,
-                       cand, nb, len, h->pd1.p, h->pidx.p, h->pd2.p);
-  HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_nn_merge<true>, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, nb,
-                     (int)splits, h->pd1.p, h->pidx.p, h->pd2.p, nn, second);
-  HIPCHK(hipGetLastError());
-  return 0;
+// Index buffers for trees of up to N nodes and up to B candidates per scan, plus the sort
+// and scan temporaries they need (shared by the plan's rounds and tcmp_nearest: nothing in
+// them outlives one index build + scan).
+int ensure_index(tcmp_handle* h, size_t N, size_t B) {
+  int rc = h->nkeys_in.ensure(N);
+  rc = rc ? rc : h->skeys.ensure(N);
+  rc = rc ? rc : h->nvals_in.ensure(N);
+  rc = rc ? rc : h->svals.ensure(N);
+  rc = rc ? rc : h->stree.ensure(N * 8);
+  rc = rc ? rc : h->stree32.ensure(N * 8);
+  rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
+  rc = rc ? rc : h->sboxf.ensure((N + 1) * 16);
+  rc = rc ? rc : h->bboxf.ensure((N / 64 + 2) * 16);
+  rc = rc ? rc : h->cflag.ensure(N);
+  rc = rc ? rc : h->cid.ensure(N);
+  rc = rc ? rc : h->cstart.ensure(N + 1);
+  rc = rc ? rc : h->sflag.ensure(N);
+  rc = rc ? rc : h->sid.ensure(N);
+  rc = rc ? rc : h->sstart.ensure(N + 1);
+  rc = rc ? rc : h->ckey.ensure(N);
+  rc = rc ? rc : h->chome.ensure(2 * B);
+  rc = rc ? rc : h->ckeys_in.ensure(B);
+  rc = rc ? rc : h->ckeys.ensure(B);
+  rc = rc ? rc : h->cvals_in.ensure(B);
+  rc = rc ? rc : h->cperm.ensure(B);
+  if (rc) return rc;
+  size_t t1 = 0, t2 = 0, t3 = 0;
+  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t1, h->nkeys_in.p, h->skeys.p, h->nvals_in.p,
+                                             h->svals.p, N, 0, 64, h->stream));
+  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t2, h->ckeys_in.p, h->ckeys.p, h->cvals_in.p,
+                                             h->cperm.p, B, 0, 64, h->stream));
+  HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, h->cflag.p, h->cid.p, (int)N, h->stream));
+  return h->sort_tmp.ensure(std::max(std::max(t1, t2), t3));
 }
 
-// Morton-chunked nearest over the plan's tree snapshot (T <= T_bound nodes on the device)
-int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_bound, int nb) {
+// Exact nearest node of nb candidates (rows of 8) among the st->n_nodes <= T_bound tree rows
+// cfg (rows of 8): the radix-tree cell index (tcmp_nn.h), then k_nearest_wave32.  Outputs:
+// nn (index), second (a lower bound of the second-smallest score, the rewire test's input),
+// score (nullable: the winner's exact fp64 score).  The plan's rounds and tcmp_nearest both
+// come here; st is the plan's state or st_nn.
+int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const double* cfg,
+                   long long T_bound, const double* cand, int nb, int* nn, double* second,
+                   double* score) {
   hipLaunchKernelGGL(k_node_keys, dim3(std::min<unsigned>(grid_for(T_bound, 256), 4096)), dim3(256),
-                     0, h->stream, h->st, h->cfg.p, T_bound, h->nkeys_in.p, h->nvals_in.p);
+                     0, h->stream, st, cfg, T_bound, h->nkeys_in.p, h->nvals_in.p);
   HIPCHK(hipGetLastError());
   size_t tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
                                              h->nvals_in.p, h->svals.p, (size_t)T_bound, 0,
                                              kKeyBits + 1, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
-  hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, h->st,
-                     h->cfg.p, h->svals.p, h->stree.p, h->stree32.p);
+  hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, st,
+                     cfg, h->svals.p, h->stree.p, h->stree32.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemsetAsync(h->cflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
   hipLaunchKernelGGL(k_nn_cut<kNnC>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     &h->st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
+                     &st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
   HIPCHK(hipGetLastError());
   tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->cflag.p, h->cid.p, (int)T_bound,
                                           h->stream));
   hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     &h->st->n_nodes, (const int*)nullptr, h->cflag.p, h->cid.p, h->cstart.p,
-                     &h->st->nn_cells);
+                     &st->n_nodes, (const int*)nullptr, h->cflag.p, h->cid.p, h->cstart.p,
+                     &st->nn_cells);
   HIPCHK(hipGetLastError());
   // one wave per cell; the cell count is device-side, so cover the worst case (one per node)
   hipLaunchKernelGGL(k_nn_cell_boxes, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0, h->stream,
-                     h->st, h->stree.p, h->cstart.p, h->skeys.p, h->cboxf.p, h->ckey.p);
+                     st, h->stree.p, h->cstart.p, h->skeys.p, h->cboxf.p, h->ckey.p);
   HIPCHK(hipGetLastError());
   // super-cells: the same radix-tree cut over the cells' first keys
   HIPCHK(hipMemsetAsync(h->sflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
   hipLaunchKernelGGL(k_nn_cut<kNnS>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     (const long long*)nullptr, &h->st->nn_cells, h->ckey.p, h->sflag.p);
+                     (const long long*)nullptr, &st->nn_cells, h->ckey.p, h->sflag.p);
   HIPCHK(hipGetLastError());
   tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->sflag.p, h->sid.p, (int)T_bound,
                                           h->stream));
   hipLaunchKernelGGL(k_nn_starts, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     (const long long*)nullptr, &h->st->nn_cells, h->sflag.p, h->sid.p,
-                     h->sstart.p, &h->st->nn_supers);
+                     (const long long*)nullptr, &st->nn_cells, h->sflag.p, h->sid.p,
+                     h->sstart.p, &st->nn_supers);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0,
-                     h->stream, h->st, h->sstart.p, h->cboxf.p, h->sboxf.p);
+                     h->stream, st, h->sstart.p, h->cboxf.p, h->sboxf.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_nn_build_blocks, dim3(grid_for(T_bound + 128, 256)), dim3(256), 0,
-                     h->stream, h->st, h->sboxf.p, h->bboxf.p);
+                     h->stream, st, h->sboxf.p, h->bboxf.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->cand.p, nb,
+  hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, cand, nb,
                      h->ckeys_in.p, h->cvals_in.p);
   HIPCHK(hipGetLastError());
   // candidates only need locality (the scan order never changes a result): top 16 key bits
@@ -1107,25 +1011,25 @@ int launch_nearest_chunked(tcmp_handle* h, const PlanParams& P, long long T_boun
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                              h->cvals_in.p, h->cperm.p, (size_t)nb,
                                              kKeyBits + 1 - 16, kKeyBits + 1, h->stream));
-  hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->st,
+  hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
                      h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave
-  HIPCHK(hipMemsetAsync(&h->st->nn_counter, 0, sizeof(int), h->stream));
-  HIPCHK(hipMemsetAsync(h->st->nn_queue, 0, sizeof(int) * 8, h->stream));
+  HIPCHK(hipMemsetAsync(&st->nn_counter, 0, sizeof(int), h->stream));
+  HIPCHK(hipMemsetAsync(st->nn_queue, 0, sizeof(int) * 8, h->stream));
   const long long waves = std::min<long long>(nb, (long long)h->cu_count * h->nn_waves_per_cu);
   const int per_wave = (int)((nb + waves - 1) / waves);
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
   h->mark_begin(F_NNSCAN, &e0);
   if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, h->cand.p, h->cperm.p,
-                       h->chome.p, nb, h->nn.p, h->second.p);
+    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
+                       h->chome.p, nb, nn, second, score);
   else
-    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, h->st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, h->cand.p, h->cperm.p,
-                       h->chome.p, nb, h->nn.p, h->second.p);
+    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
+                       h->chome.p, nb, nn, second, score);
   HIPCHK(hipGetLastError());
   h->mark_end(F_NNSCAN, e0);
   return 0;
@@ -1175,6 +1079,7 @@ PlanParams default_params() {
   P.goal_tol = 1e-2;
   P.uniform_w = 1;
   P.max_nodes = LLONG_MAX;
+  P.nn_cmax = 8.0;  // planner configurations lie in the joint-limit box (|q| <= 3.7525)
   return P;
 }
 
@@ -1194,7 +1099,8 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  for (int i = 0; i < n; ++i) out[i] = s.prof[i];
+  // prof[] has 16 entries; 12..35 are the exact-test stats of TCMP_PROF_EXACT builds
+  for (int i = 0; i < n; ++i) out[i] = i < 16 ? s.prof[i] : 0;
 #ifdef TCMP_PROF_EXACT
   unsigned long long ex[24];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
@@ -1286,8 +1192,8 @@ int tcmp_create(int device, tcmp_handle** out) {
   }
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
-  const char* nb_env = getenv("TCMP_NN_BRUTE");
-  h->nn_brute = nb_env && nb_env[0] == '1';
+  HIPCHK(hipMalloc(&h->st_nn, sizeof(DevState)));
+  HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   *out = h;
   return 0;
@@ -1315,10 +1221,9 @@ int tcmp_destroy(tcmp_handle* h) {
                   &h->s1, &h->s2, &h->s3})
     b->release();
   for (auto* b : {&h->parent, &h->nn, &h->nsafe, &h->nsteps, &h->nbr, &h->ncount, &h->i0,
-                  &h->i1, &h->i2, &h->pidx, &h->rwlist})
+                  &h->i1, &h->i2, &h->rwlist})
     b->release();
-  h->pd1.release();
-  h->pd2.release();
+  h->nnscore.release();
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
   for (auto* b : {&h->nvals_in, &h->svals, &h->cvals_in, &h->cperm}) b->release();
   h->stree.release();
@@ -1349,6 +1254,7 @@ int tcmp_destroy(tcmp_handle* h) {
   }
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->st) (void)hipFree(h->st);
+  if (h->st_nn) (void)hipFree(h->st_nn);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -1828,26 +1734,51 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
 int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* samples,
                  int64_t n, const double* weights, int32_t* idx) {
   if (int rc = set_dev(h)) return rc;
-  if (T <= 0 || n < 0 || n > INT_MAX || !tree || (n > 0 && (!samples || !idx)))
+  if (T <= 0 || T > INT_MAX || n < 0 || n > INT_MAX || !tree || (n > 0 && (!samples || !idx)))
     return fail(-1, "bad arguments");
   if (n == 0) return 0;
-  int rc = upload7(h, h->s0, tree, T);
-  rc = rc ? rc : upload7(h, h->s1, samples, n);
-  rc = rc ? rc : h->i0.ensure((size_t)n);
-  rc = rc ? rc : h->cgoal.ensure((size_t)n);
-  if (rc) return rc;
   PlanParams P = default_params();
   bool uw = true;
   if (weights) {
     for (int k = 0; k < 7; ++k) {
+      if (!(weights[k] > 0) || !std::isfinite(weights[k])) return fail(-1, "weights must be positive");
       P.w[k] = weights[k];
       uw &= weights[k] == weights[0];
     }
   }
   P.uniform_w = uw ? 1 : 0;
-  if ((rc = launch_nearest(h, P, h->s0.p, T, T, h->s1.p, (int)n, h->i0.p, nullptr))) return rc;
+  // the scan's fp32 error terms need a bound on |q| (8 covers the joint-limit box)
+  double cmax = 8.0;
+  for (long long i = 0; i < 7 * T; ++i) {
+    if (!std::isfinite(tree[i])) return fail(-1, "non-finite tree coordinate");
+    cmax = std::max(cmax, fabs(tree[i]));
+  }
+  for (long long i = 0; i < 7 * n; ++i) {
+    if (!std::isfinite(samples[i])) return fail(-1, "non-finite sample coordinate");
+    cmax = std::max(cmax, fabs(samples[i]));
+  }
+  P.nn_cmax = cmax * (1.0 + 1e-6);
+  int rc = upload7(h, h->s0, tree, T);
+  rc = rc ? rc : upload7(h, h->s1, samples, n);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  rc = rc ? rc : h->s2.ensure((size_t)n);
+  rc = rc ? rc : ensure_index(h, (size_t)T, (size_t)n);
+  if (rc) return rc;
+  DevState s;
+  memset(&s, 0, sizeof(s));
+  s.n_nodes = T;
+  HIPCHK(hipMemcpyAsync(h->st_nn, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
+  const size_t ev_before = h->ev_used.size();
+  rc = launch_nearest(h, P, h->st_nn, h->s0.p, T, h->s1.p, (int)n, h->i0.p, h->s2.p, nullptr);
+  if (rc) return rc;
   HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
+  // the scan's timing events belong to no plan
+  while (h->ev_used.size() > ev_before) {
+    h->ev_pool.push_back(h->ev_used.back().a);
+    h->ev_pool.push_back(h->ev_used.back().b);
+    h->ev_used.pop_back();
+  }
   return 0;
 }
 
@@ -1947,39 +1878,8 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->ncount.ensure(B);
   rc = rc ? rc : h->second.ensure(B);
   rc = rc ? rc : h->rwlist.ensure(B);
-  rc = rc ? rc : h->nkeys_in.ensure(N);
-  rc = rc ? rc : h->skeys.ensure(N);
-  rc = rc ? rc : h->nvals_in.ensure(N);
-  rc = rc ? rc : h->svals.ensure(N);
-  rc = rc ? rc : h->stree.ensure(N * 8);
-  rc = rc ? rc : h->stree32.ensure(N * 8);
-  rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
-  rc = rc ? rc : h->sboxf.ensure((N + 1) * 16);
-  rc = rc ? rc : h->bboxf.ensure((N / 64 + 2) * 16);
-  rc = rc ? rc : h->cflag.ensure(N);
-  rc = rc ? rc : h->cid.ensure(N);
-  rc = rc ? rc : h->cstart.ensure(N + 1);
-  rc = rc ? rc : h->sflag.ensure(N);
-  rc = rc ? rc : h->sid.ensure(N);
-  rc = rc ? rc : h->sstart.ensure(N + 1);
-  rc = rc ? rc : h->ckey.ensure(N);
-  rc = rc ? rc : h->chome.ensure(2 * B);
-  rc = rc ? rc : h->ckeys_in.ensure(B);
-  rc = rc ? rc : h->ckeys.ensure(B);
-  rc = rc ? rc : h->cvals_in.ensure(B);
-  rc = rc ? rc : h->cperm.ensure(B);
-  if (!rc) {
-    size_t t1 = 0, t2 = 0;
-    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t1, h->nkeys_in.p, h->skeys.p,
-                                               h->nvals_in.p, h->svals.p, (size_t)N, 0, 64,
-                                               h->stream));
-    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t2, h->ckeys_in.p, h->ckeys.p,
-                                               h->cvals_in.p, h->cperm.p, (size_t)B, 0, 64,
-                                               h->stream));
-    size_t t3 = 0;
-    HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, h->cflag.p, h->cid.p, (int)N, h->stream));
-    rc = h->sort_tmp.ensure(std::max(std::max(t1, t2), t3));
-  }
+  rc = rc ? rc : h->nnscore.ensure(B);
+  rc = rc ? rc : ensure_index(h, N, B);
   rc = rc ? rc : h->i0.ensure(2);
   if (rc) return rc;
   h->max_batch = cfg->max_batch;
@@ -2048,11 +1948,11 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   // the snapshot holds at most 1 + (samples issued before this round) nodes
   {
     const long long T_bound = 1 + h->samples_issued - nb;
-    const int rc = h->nn_brute
-                       ? launch_nearest(h, P, h->cfg.p, T_bound, -1, h->cand.p, nb, h->nn.p, h->second.p)
-                       : launch_nearest_chunked(h, P, T_bound, nb);
-    if (rc) return rc;
+    if (int rc = launch_nearest(h, P, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
+                                h->second.p, h->nnscore.p))
+      return rc;
   }
+  h->last_nb = nb;
   h->mark_end(F_NEAREST, e0);
   h->launches_nearest++;
   h->mark_begin(F_EDGES, &e0);
@@ -2242,6 +2142,33 @@ int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32
       for (int k = 0; k < 7; ++k) cfg[7 * i + k] = tmp[8 * i + k];
     if (cost) cost[i] = tmp[8 * i + 7];
   }
+  return 0;
+}
+
+int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn,
+                          double* score, int64_t* snap, int32_t* nb) {
+  if (int rc = set_dev(h)) return rc;
+  if (!snap || !nb || cap < 0) return fail(-1, "bad arguments");
+  if (!h->plan_open) return fail(-1, "no open plan");
+  long long T = 0;
+  HIPCHK(hipMemcpyAsync(&T, &h->st->snap, sizeof(T), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *snap = T;
+  *nb = h->last_nb;
+  const long long m = std::min<long long>(cap, h->last_nb);
+  if (m <= 0) return 0;
+  if (cand) {
+    std::vector<double> tmp((size_t)m * 8);
+    HIPCHK(hipMemcpyAsync(tmp.data(), h->cand.p, tmp.size() * sizeof(double),
+                          hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(hipStreamSynchronize(h->stream));
+    for (long long i = 0; i < m; ++i)
+      for (int k = 0; k < 7; ++k) cand[7 * i + k] = tmp[8 * i + k];
+  }
+  if (nn) HIPCHK(hipMemcpyAsync(nn, h->nn.p, m * sizeof(int), hipMemcpyDeviceToHost, h->stream));
+  if (score)
+    HIPCHK(hipMemcpyAsync(score, h->nnscore.p, m * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
 

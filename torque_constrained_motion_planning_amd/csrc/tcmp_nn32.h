@@ -6,8 +6,9 @@
 // arithmetic as k_nearest_wave, so the winner and its distance are bit-identical) only when
 // its fp32 value r32 could belong to a node at least as close as the wave's current best m:
 //
-//   |q| <= kNnCoordMax on the search path (joint-limit box), so each fp32 coordinate
-//   difference is within e = 4 u kNnCoordMax of the exact one (u = 2^-24), and with
+//   |q| <= cmax (P.nn_cmax: 8 > the joint-limit magnitude 3.7525 on the planner's path; the
+//   data's own bound for tcmp_nearest), so each fp32 coordinate difference is within
+//   e = 4 u cmax of the exact one (u = 2^-24), and with
 //   D = exact weighted distance, E = e sqrt(sum w):   r32 <= (1 + g) (D + E)^2,  g = 16 u.
 //   Refine iff r32 <= R(m) = (1 + g)(sqrt(m) + E)^2 (rounded up, with slack).
 //
@@ -23,8 +24,6 @@
 #pragma once
 
 constexpr double kNnU32 = 5.9604644775390625e-08;  // 2^-24
-constexpr double kNnCoordMax = 8.0;                 // > joint-limit magnitude (3.7525)
-constexpr double kNnE = 4.0 * kNnU32 * kNnCoordMax;
 constexpr double kNnG = 16.0 * kNnU32;
 
 __device__ __forceinline__ unsigned xcc_id() {
@@ -34,11 +33,13 @@ __device__ __forceinline__ unsigned xcc_id() {
 }
 
 // Lower bound of the weighted squared distance from s to a float box, in fp32, never above
-// the fp64 value box_lb<UW> would give: each gap is shrunk by 1e-6 (> the fp32 rounding of
-// s and of the subtraction for |q| <= kNnCoordMax) and the sum by 1e-6 relative.
+// the exact value: each gap is shrunk by `gap` = 1.25e-7 cmax (> the fp32 rounding of s and
+// of the subtraction for |q| <= cmax; 1e-6 on the planner's path) and the sum by 1e-6
+// relative.
 template <bool UW>
 __device__ __forceinline__ float box_lb32(const float* b, const float s[7], const float w[7],
-                                          int* start = nullptr, int* count = nullptr) {
+                                          float gap, int* start = nullptr,
+                                          int* count = nullptr) {
   const float4 l0 = *reinterpret_cast<const float4*>(b);
   const float4 l1 = *reinterpret_cast<const float4*>(b + 4);
   const float4 h0 = *reinterpret_cast<const float4*>(b + 8);
@@ -50,7 +51,7 @@ __device__ __forceinline__ float box_lb32(const float* b, const float s[7], cons
   float lb = 0.f;
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
-    const float g = fmaxf(0.f, fmaxf(lo[k] - s[k], s[k] - hi[k]) - 1e-6f);
+    const float g = fmaxf(0.f, fmaxf(lo[k] - s[k], s[k] - hi[k]) - gap);
     lb = fmaf(UW ? g : w[k] * g, g, lb);
   }
   return lb * 0.999999f;
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
                                                         const float* sbox, const float* bbox,
                                                         const double* cand,
                                                         const int* cperm, const int* home, int nb,
-                                                        int* nn, double* second) {
+                                                        int* nn, double* second, double* score) {
   const int lane = lane_id();
   const long long T = st->n_nodes;
   const int nch = st->nn_cells, nsup = st->nn_supers;
@@ -78,7 +79,8 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     w32[k] = (float)w[k];
     wsum += w[k];
   }
-  const double E = kNnE * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
+  const double E = 4.0 * kNnU32 * P.nn_cmax * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
+  const float gap = (float)(1.25e-7 * P.nn_cmax);
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
   const float E32 = __double2float_ru(E * (1.0 + 1e-9)), ru32 = __double2float_ru(ru);
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
@@ -233,7 +235,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
     for (int gb = 0; gb < nblk; gb += 64) {
       const int bidx = zigzag(hb, gb + lane, nblk);
-      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, s32, w32) : INFINITY;
+      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, s32, w32, gap) : INFINITY;
       tests += (unsigned long long)min(64, nblk - gb);
       uint64_t bmask = __ballot(lbb <= thr);
       while (bmask) {
@@ -245,7 +247,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
         const int sidx = 64 * blk + ((lane + rot) & 63);
         int sc0 = 0, scn = 0;
         const float lbs =
-            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, &sc0, &scn) : INFINITY;
+            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, gap, &sc0, &scn) : INFINITY;
         tests += (unsigned long long)min(64, nsup - 64 * blk);
         uint64_t smask = __ballot(lbs <= thr);
         NN_TICK(1);
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
           const int c = S0 + lane;
           const bool cv = lane < Sn && c != hc;
           int cst = 0, ccn = 0;
-          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, &cst, &ccn) : INFINITY;
+          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, gap, &cst, &ccn) : INFINITY;
           tests += (unsigned long long)Sn;
           uint64_t cmask = __ballot(lbc <= thr);
           NN_TICK(2);
@@ -296,6 +298,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
     if (lane == 0) {
       nn[lj] = wi == INT_MAX ? 0 : wi;
       if (second) second[lj] = sec;
+      if (score) score[lj] = m;
     }
     NN_TICK(4);
   }
