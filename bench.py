@@ -10,7 +10,9 @@ final validation.  Synthetic scene, seed = 1234 + query id.
 
 N > 1 (torchrun, one process per GPU): every rank plans its own queries (independent
 queries shard with no data-path collective, scaling "weak"); solved trajectories are
-gathered to rank 0 over RCCL at the end of each step, as in configs[3].
+gathered to rank 0 over RCCL at the end of each step, as in configs[3].  The collectives
+(barrier, max-over-ranks time, the trajectory gather) are libtcmp.so's own RCCL
+communicator (tcmp_dist_*, tcmp_gather_paths): no PyTorch in this process.
 
 Prints ONE JSON line on rank 0.
 """
@@ -39,12 +41,13 @@ NN_FLOP_PER_PAIR = 21       # 7 sub + 7 fma per (candidate, node) pair, fp32 fir
 F_FK, F_BP, F_RNE_STATIC, F_SAT, N_LINKS = 720, 48, 3000, 260, 10
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of this
-    workload (profiles/*_pmc_hbm.json): 2 x FETCH_SIZE (gfx950 correction) + WRITE_SIZE."""
+def pmc_traffic(kernel, workload):
+    """HBM bytes per launch of `kernel` from the newest committed rocprofv3 PMC summary of THIS
+    workload (profiles/<tag>_pmc_hbm_<workload>.json): 2 x FETCH_SIZE (gfx950 correction) +
+    WRITE_SIZE.  None when the workload was never profiled."""
     prof = os.path.join(REPO, "profiles")
-    pmc = sorted(f for f in os.listdir(prof) if f.endswith("_pmc_hbm.json")) \
-        if os.path.isdir(prof) else []
+    suffix = "_pmc_hbm_%s.json" % workload
+    pmc = sorted(f for f in os.listdir(prof) if f.endswith(suffix)) if os.path.isdir(prof) else []
     if not pmc:
         return None
     d = json.load(open(os.path.join(prof, pmc[-1])))["dispatches"].get(kernel, [])
@@ -65,7 +68,7 @@ WORKLOADS = {
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
-               batch=262144, queries=1, scaling="weak",
+               batch=262144, alt_batch=65536, queries=1, scaling="weak",
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
@@ -76,8 +79,10 @@ WORKLOADS = {
     "c5": dict(boxes=0, meshes=256, mode=_lib.TORQUE_RNE, mass=5.0, samples=10_000_000,
                batch=262144, queries=1, scaling="strong",
                text="C5: dense clutter, 256 convex meshes (Panda link hulls scaled 0.5-1.5, "
-                    "random poses), 5 kg, rne, 1e7 samples per step split over the GPUs "
-                    "(independent replica trees of 1e7/N samples, same scene)"),
+                    "random poses), 5 kg, rne, 1e7 samples per step split over the GPUs -- "
+                    "throughput mode: N independent replica trees of 1e7/N samples on the same "
+                    "scene (smaller trees than the 1-GPU 1e7-sample tree: not the same problem "
+                    "as N grows)"),
 }
 
 
@@ -172,7 +177,7 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
         done = [json.loads(o) for o, p in zip(outs, procs) if p.returncode == 0 and o.strip()]
     multi = sum(d["samples"] for d in done) / dtw if done else None
     return {"value": multi if multi else single, "unit": "samples/s",
-            "cores": len(done) if multi else 1, "kind": "port",
+            "cores": len(done) if multi else 1, "host_nproc": os.cpu_count(), "kind": "port",
             "single_core": single,
             "sample": "oracle/tcmp_oracle.c sequential RRT* (B=1, reference loop semantics) on the "
                       "same %s: %d samples per query; single core "
@@ -195,6 +200,8 @@ def main():
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
                     help="host cores for the multi-core CPU baseline (16 = one GPU's share)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-alt", action="store_true",
+                    help="skip the SURVEY 8d default-batch line (config_alt)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--self-collisions", action="store_true",
                     help="add the arm's self-collision pairs (off in the reference planner)")
@@ -205,19 +212,9 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    # rehearsal of the N > 1 path on one GPU (TCMP_BENCH_BACKEND=gloo TCMP_BENCH_DEVICE=0:
-    # every rank on GPU 0, collectives over gloo on host tensors); the real run is nccl (RCCL)
-    backend = os.environ.get("TCMP_BENCH_BACKEND", "nccl")
-    gpu = int(os.environ.get("TCMP_BENCH_DEVICE", local_rank))
-    coll_dev = "cuda" if backend == "nccl" else "cpu"
-    if world > 1:
-        import torch
-        import torch.distributed as tdist
-        torch.cuda.set_device(gpu)
-        tdist.init_process_group(backend)
-        dist = tdist
+    gpu = int(os.environ.get("LOCAL_RANK", "0"))
+    # one process per GPU; the collectives are libtcmp.so's RCCL communicator (no torch)
+    comm = shard.comm_from_env(device=gpu) if world > 1 else None
 
     W = dict(WORKLOADS[args.workload])
     if args.samples is not None:
@@ -247,10 +244,11 @@ def main():
                           n_mesh=W["meshes"]) for q in qids]
 
     def barrier():
-        if dist is not None:
-            import torch
-            torch.cuda.synchronize()
-            dist.barrier()
+        # every engine stream of this rank drained, then the ranks meet (RCCL all-reduce)
+        for e in engines:
+            e.synchronize()
+        if comm is not None:
+            comm.barrier()
 
     step_seed = lambda s: 1234 + rank * 100003 + s  # noqa: E731
 
@@ -279,10 +277,9 @@ def main():
                       key=lambda x: x[0])
         outs = [d[2] for d in done]
         res = [d[1].as_dict() for d in done]
-        if dist is not None:
+        if comm is not None:
             # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
-            shard.gather_trajectories(dist, [shard.pack_trajectory(o) for o in outs],
-                                      labels, world, rank, device=coll_dev)
+            shard.gather_trajectories(comm, [shard.pack_trajectory(o) for o in outs], labels)
         return res
 
     for w in range(args.warmup):
@@ -295,14 +292,12 @@ def main():
         results += step(s)
     barrier()
     dt = time.perf_counter() - t0
-    if dist is not None:
-        import torch
-        t = torch.tensor([dt], device=coll_dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
+    # samples the devices actually drew (tcmp_plan_result.n_samples), summed over all ranks
+    total_samples = float(sum(x["n_samples"] for x in results))
+    if comm is not None:
+        dt = float(comm.allreduce([dt], _lib.REDUCE_MAX)[0])
+        total_samples = float(comm.allreduce([total_samples], _lib.REDUCE_SUM)[0])
     n_queries_total = W["queries"] if W["queries"] > 1 else world
-    total_samples = W["samples"] * n_queries_total * args.steps
     S = args.steps
     kernel_ms = {k: sum(x[k] for x in results) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
@@ -320,7 +315,7 @@ def main():
     roof_nn = {
         "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, launches),
         "bound": "valu_fp32", "achieved": nn_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-        "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32"),
+        "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32", args.workload),
         "algorithmic": "%d flop per evaluated (candidate, node) pair; %d pairs over %d launches "
                        "(brute force would be %d pairs: %.1f PFLOP/s equivalent)" % (
                            NN_FLOP_PER_PAIR, nn_pairs, launches, nn_full,
@@ -336,7 +331,7 @@ def main():
     roof_ed = {
         "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
         "bound": "valu_fp64", "achieved": ed_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-        "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges"),
+        "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges", args.workload),
         "algorithmic": "per extend step F_fk %d + F_bp %d x %d links x %d obstacles + F_rne %d, "
                        "+ F_sat %d per pair past the cull; %d steps, %d such pairs, %d launches" % (
                            F_FK, F_BP, N_LINKS, n_obs_total, f_rne, F_SAT, steps, sat,
@@ -384,10 +379,33 @@ def main():
         line["cpu_baseline"] = cpu_baseline(obs, goal, cpu_n, step_seed(0), args.cpu_workers,
                                             mode, mass, meshes=pack,
                                             what=W["text"].split(",")[0] + " scene")
+    if rank == 0 and world == 1 and W.get("alt_batch") and not args.no_alt:
+        # the same workload at SURVEY 8d's default batch, beside the headline's tuned batch
+        # (the batch changes the tree: more, smaller rounds see fresher snapshots)
+        alt = dict(W, batch=W["alt_batch"])
+        obs, pack, goal = queries[0]
+        for w in range(args.warmup):
+            run_query(eng, obs, goal, alt["samples"], alt["batch"], step_seed(20_000 + w), mode,
+                      mass, meshes=pack)
+        eng.synchronize()
+        t1 = time.perf_counter()
+        alt_res = [run_query(eng, obs, goal, alt["samples"], alt["batch"], step_seed(s), mode,
+                             mass, meshes=pack)[0].as_dict() for s in range(args.steps)]
+        eng.synchronize()
+        dta = time.perf_counter() - t1
+        line["config_alt"] = {
+            "batch_per_round": alt["batch"], "steps": args.steps,
+            "value": sum(x["n_samples"] for x in alt_res) / dta, "unit": "samples/s",
+            "ms_per_step": dta / args.steps * 1e3,
+            "edge_steps_per_sample": sum(x["edge_steps"] for x in alt_res) /
+            max(1, sum(x["n_samples"] for x in alt_res)),
+            "note": "SURVEY 8d default batch; the headline line runs batch_per_round %d" % W["batch"]}
+        line["config"]["edge_steps_per_sample"] = steps / max(1.0, float(
+            sum(x["n_samples"] for x in results)))
     if rank == 0:
         print(json.dumps(line), flush=True)
-    if dist is not None:
-        dist.destroy_process_group()
+    if comm is not None:
+        comm.close()
     eng.close()
 
 

@@ -40,6 +40,8 @@ int tcmp_destroy(tcmp_handle* h);
 const char* tcmp_last_error(void);
 int tcmp_device_count(int* n);
 int tcmp_version(void);
+/* wait for all work queued on the handle's HIP stream */
+int tcmp_synchronize(tcmp_handle* h);
 /* profiling builds (-DTCMP_PROF) only: k_edges clock breakdown accumulated since create
  * (total, work fetch, collision, torque, bookkeeping, tier-4 exact, ...) and exact-test
  * outcome counts and mesh-stage clocks (12..35), n <= 36; zeros otherwise. */
@@ -222,6 +224,45 @@ int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32
  * The first min(cap, nb) rows are copied; any array pointer may be NULL. */
 int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn,
                           double* score, int64_t* snap, int32_t* nb);
+
+/* ---- multi-GPU: query sharding + RCCL gather of solved paths -------------- */
+/* One process per GPU; independent queries are dealt to ranks (collect_data.py:74-85 plans
+ * them in a loop); the only collective is the gather of solved trajectories to rank 0.
+ * A trajectory row is [q(7) qd(7) qdd(7) dt(1)] (Conf values / velocities / accelerations /
+ * dt of create_trajectory, utils.py:3340-3347). */
+#define TCMP_TRAJ_COLS 22
+#define TCMP_REDUCE_SUM 0
+#define TCMP_REDUCE_MAX 1
+typedef struct tcmp_comm tcmp_comm;
+
+/* TCP rendezvous: rank 0 listens on addr:port and sends its nbytes `blob` to every other
+ * rank (which connect, retrying until timeout_ms).  Host only, no GPU.  Used for the
+ * ncclUniqueId; world == 1 returns at once. */
+int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port, void* blob,
+                    int32_t nbytes, int32_t timeout_ms);
+
+/* communicator of `world` ranks over RCCL on HIP device `device` (rank 0's unique id through
+ * tcmp_rendezvous at addr:port).  world == 1: no RCCL communicator, no GPU touched. */
+int tcmp_dist_init(int32_t rank, int32_t world, int32_t device, const char* addr, int32_t port,
+                   tcmp_comm** out);
+int tcmp_dist_destroy(tcmp_comm* c);
+int tcmp_dist_rank(const tcmp_comm* c, int32_t* rank, int32_t* world);
+/* device-synchronise this rank, then an RCCL all-reduce as the barrier */
+int tcmp_dist_barrier(tcmp_comm* c);
+/* in-place all-reduce of n doubles (op TCMP_REDUCE_SUM / TCMP_REDUCE_MAX) */
+int tcmp_dist_allreduce(tcmp_comm* c, double* v, int32_t n, int32_t op);
+/* all-gather of n int64 per rank: out = world x n, rank order */
+int tcmp_dist_allgather_i64(tcmp_comm* c, const int64_t* in, int32_t n, int64_t* out);
+
+/* gather every rank's solved paths to rank 0 (ncclGroupStart; ncclSend/ncclRecv;
+ * ncclGroupEnd after a size all-gather).  In: n_local paths, ids[i], rows[i], data = the
+ * paths' rows concatenated (sum(rows) x TCMP_TRAJ_COLS).  Out, rank 0 only: n_queries paths
+ * in rank order (out_ids, out_rows) with their rows concatenated in out_data; elsewhere
+ * n_queries = n_rows = 0.  Capacities too small: status -4 with n_queries / n_rows set (the
+ * collective still completes on every rank).  Collective: every rank must call it. */
+int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const int64_t* rows,
+                      const double* data, int64_t cap_queries, int64_t cap_rows, int64_t* out_ids,
+                      int64_t* out_rows, double* out_data, int64_t* n_queries, int64_t* n_rows);
 
 #ifdef __cplusplus
 }

@@ -342,9 +342,19 @@ def search(name, rng, n_obs, mode, mass, exec_time, iters, seed, want_found=True
     raise RuntimeError("no golden query for " + name)
 
 
+def gen_c1k():
+    """C1 at BASELINE configs[0]'s own size: empty scene, 0 kg, base, 1000 RRT* iterations,
+    T_exec 5 (the goal is reached at it=1 and the loop runs on to 1000)."""
+    run_reference("c1_1k_base", TOP_HOLDING_LEFT_ARM, (0.5, 0.2, 0.1, -1.5, 0.3, 1.8, 0.2),
+                  [], "base", 0.0, 5.0, 1000, 0, stride=37)
+
+
 def main():
     if "--only-fk" in sys.argv:
         gen_fk(os.path.join(HERE, "fk_golden.npz"))
+        return
+    if "--only-c1k" in sys.argv:
+        gen_c1k()
         return
     gen_fk(os.path.join(HERE, "fk_golden.npz"))
     gen_rne(os.path.join(HERE, "rne_golden.npz"))
@@ -353,6 +363,7 @@ def main():
     # C1-like: empty scene, base, straight edge succeeds (SURVEY App. C goal), T_exec 5
     run_reference("c1_base_direct", TOP_HOLDING_LEFT_ARM, (0.5, 0.2, 0.1, -1.5, 0.3, 1.8, 0.2),
                   [], "base", 0.0, 5.0, 60, 0, stride=37)
+    gen_c1k()
     # empty scene, torque-blocked straight edge -> tree growth
     search("empty_rne5", rng, 0, "rne", 5.0, 1.0, 300, 1, random_start=True)
     search("empty_nov5", rng, 0, "nov", 5.0, 1.0, 300, 2, random_start=True)

@@ -1,6 +1,13 @@
-"""CPU, world_size 2 (gloo): the multi-GPU sharding path -- round-robin query deal and the
-gather of solved trajectories to rank 0 (bench.py / shard.py).  The per-rank planner here is
-the CPU oracle (the GPU engine runs the same queries in the gpu tests)."""
+"""CPU, world size 2 and 4: the multi-GPU sharding path without a GPU.
+
+* tcmp_rendezvous (the TCP hand-off of rank 0's RCCL unique id, libtcmp.so) between real
+  processes;
+* tcmp_gather_paths' packing and unpacking through the C-ABI (a one-rank communicator needs
+  no RCCL and touches no GPU);
+* the 2-rank shard path: round-robin deal, per-rank planning (the CPU oracle stands in for the
+  GPU engine), the wire form of tcmp_gather_paths, with gloo moving the packed buffers the
+  way RCCL's send/recv does on the GPU -- torch appears only in this test harness.
+"""
 import os
 import socket
 import sys
@@ -19,22 +26,59 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, n_queries, q):
+def _rdzv_worker(rank, world, port, blob, q):
     sys.path.insert(0, REPO)
-    sys.path.insert(0, os.path.join(REPO, "oracle"))
-    import torch.distributed as dist
-    import oracle as O
-    from torque_constrained_motion_planning_amd import shard
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    ids = shard.queries_for_rank(n_queries, world, rank)
-    trajs = [shard.pack_trajectory(_plan(O, i)) for i in ids]
-    res = shard.gather_trajectories(dist, trajs, ids, world, rank)
-    if rank == 0:
-        q.put({k: v for k, v in res.items()})
-    dist.barrier()
-    dist.destroy_process_group()
+    from torque_constrained_motion_planning_amd import _lib
+    got = _lib.rendezvous(rank, world, "127.0.0.1", port, blob if rank == 0 else bytes(len(blob)),
+                          timeout_ms=60000)
+    q.put((rank, got))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_rendezvous_processes(world):
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    blob = np.random.default_rng(world).bytes(128)  # the size of an ncclUniqueId
+    procs = [ctx.Process(target=_rdzv_worker, args=(r, world, port, blob, q))
+             for r in reversed(range(world))]  # non-root ranks first: they must retry
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert sorted(got) == list(range(world))
+    assert all(v == blob for v in got.values())
+
+
+def test_rendezvous_rejects_bad_arguments():
+    sys.path.insert(0, REPO)
+    from torque_constrained_motion_planning_amd import _lib
+    with pytest.raises(_lib.TcmpError):
+        _lib.rendezvous(2, 2, "127.0.0.1", 1234, b"x" * 8)
+    assert _lib.rendezvous(0, 1, "127.0.0.1", 1234, b"abc") == b"abc"
+
+
+def test_gather_paths_capi_one_rank():
+    """tcmp_gather_paths packing/unpacking through the C-ABI (world 1: local copy)."""
+    from torque_constrained_motion_planning_amd import _lib, shard
+    comm = _lib.Comm(0, 1, 0)
+    rng = np.random.default_rng(5)
+    trajs = [rng.normal(size=(7, 22)), np.zeros((0, 22)), rng.normal(size=(3, 22))]
+    got = shard.gather_trajectories(comm, trajs, [9, 4, 1])
+    assert sorted(got) == [1, 4, 9]
+    assert np.array_equal(got[9], trajs[0]) and np.array_equal(got[1], trajs[2])
+    assert got[4].shape == (0, 22)
+    # too small an output: status -4 after the collective, sizes reported
+    ids, rows, data = shard.pack_paths(trajs, [9, 4, 1])
+    with pytest.raises(_lib.TcmpError, match="capacity"):
+        comm.gather_paths(ids, rows, data, 3, 5)
+    assert (comm.allreduce([2.0, -1.0], _lib.REDUCE_MAX) == [2.0, -1.0]).all()
+    assert (comm.allgather_i64([3, 4]) == [[3, 4]]).all()
+    comm.barrier()
+    comm.close()
 
 
 def _plan(O, qid):
@@ -44,6 +88,44 @@ def _plan(O, qid):
     if r["status"] != 0:
         return None
     return r
+
+
+def _shard_worker(rank, world, port, n_queries, q):
+    sys.path.insert(0, REPO)
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import torch
+    import torch.distributed as dist
+    import oracle as O
+    from torque_constrained_motion_planning_amd import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ids_local = shard.queries_for_rank(n_queries, world, rank)
+    ids, rows, data = shard.pack_paths([shard.pack_trajectory(_plan(O, i)) for i in ids_local],
+                                       ids_local)
+    # tcmp_gather_paths' exchange: sizes all-gathered, then each rank's header and body to 0
+    sizes = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([len(ids), int(rows.sum())], dtype=torch.int64))
+    hdr = torch.from_numpy(np.stack([ids, rows], 1).reshape(-1).copy())
+    body = torch.from_numpy(data.reshape(-1).copy())
+    if rank == 0:
+        hs, bs = [hdr], [body]
+        for r in range(1, world):
+            nq, nr = (int(x) for x in sizes[r])
+            h = torch.zeros(2 * nq, dtype=torch.int64)
+            b = torch.zeros(22 * nr, dtype=torch.float64)
+            dist.recv(h, src=r)
+            dist.recv(b, src=r)
+            hs.append(h)
+            bs.append(b)
+        H = torch.cat(hs).numpy().reshape(-1, 2)
+        got = shard.unpack_paths(H[:, 0], H[:, 1], torch.cat(bs).numpy().reshape(-1, 22))
+        q.put(got)
+    else:
+        dist.send(hdr, dst=0)
+        dist.send(body, dst=0)
+    dist.barrier()
+    dist.destroy_process_group()
 
 
 def test_round_robin_deal():
@@ -72,7 +154,7 @@ def test_gather_two_ranks_gloo():
     q = ctx.Queue()
     port = _free_port()
     n_queries = 5
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, n_queries, q)) for r in range(2)]
+    procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, n_queries, q)) for r in range(2)]
     for p in procs:
         p.start()
     got = q.get(timeout=240)

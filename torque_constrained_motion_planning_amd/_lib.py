@@ -23,12 +23,17 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 # C-ABI surface declared in include/tcmp.h (tests check the library exports all of them)
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
+    "tcmp_synchronize",
     "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters",
+    "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
+    "tcmp_dist_barrier", "tcmp_dist_allreduce", "tcmp_dist_allgather_i64", "tcmp_gather_paths",
 ]
+TRAJ_COLS = 22
+REDUCE_SUM, REDUCE_MAX = 0, 1
 
 
 class PlanCfg(ctypes.Structure):
@@ -91,6 +96,7 @@ def load_library(path=LIB_PATH):
         L.tcmp_create.argtypes = [ctypes.c_int, ctypes.POINTER(vp)]
         L.tcmp_destroy.argtypes = [vp]
         L.tcmp_device_count.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        L.tcmp_synchronize.argtypes = [vp]
         L.tcmp_set_scene.argtypes = [vp, _dp, ctypes.c_int32]
         L.tcmp_set_meshes.argtypes = [vp, _dp, _i32p, _dp, _i32p, _i32p, _i32p, _dp, ctypes.c_int32]
         L.tcmp_set_mesh_lods.argtypes = [vp, ctypes.POINTER(Hulls), ctypes.POINTER(Hulls),
@@ -116,6 +122,16 @@ def load_library(path=LIB_PATH):
         L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
         L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
         L.tcmp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
+        i32 = ctypes.c_int32
+        L.tcmp_rendezvous.argtypes = [i32, i32, ctypes.c_char_p, i32, vp, i32, i32]
+        L.tcmp_dist_init.argtypes = [i32, i32, i32, ctypes.c_char_p, i32, ctypes.POINTER(vp)]
+        L.tcmp_dist_destroy.argtypes = [vp]
+        L.tcmp_dist_rank.argtypes = [vp, _i32p, _i32p]
+        L.tcmp_dist_barrier.argtypes = [vp]
+        L.tcmp_dist_allreduce.argtypes = [vp, _dp, i32, i32]
+        L.tcmp_dist_allgather_i64.argtypes = [vp, _i64p, i32, _i64p]
+        L.tcmp_gather_paths.argtypes = [vp, i32, _i64p, _i64p, _dp, ctypes.c_int64,
+                                        ctypes.c_int64, _i64p, _i64p, _dp, _i64p, _i64p]
         _lib = L
         return L
 
@@ -169,6 +185,9 @@ class Engine:
             self.close()
         except Exception:
             pass
+
+    def synchronize(self):
+        self._check(self.L.tcmp_synchronize(self.h))
 
     # ---- scene ------------------------------------------------------------------------
     def set_scene(self, obb, meshes=None):
@@ -368,6 +387,77 @@ class Engine:
                                                  ctypes.byref(snap), ctypes.byref(nb)))
         m = min(cap, nb.value)
         return cand[:m], nn[:m], score[:m], snap.value
+
+
+def check(rc):
+    if rc != 0:
+        raise TcmpError("tcmp error %d: %s" % (rc, load_library().tcmp_last_error().decode()))
+
+
+class Comm:
+    """tcmp_comm: the ranks of a multi-GPU job (one process per GPU) over RCCL; world == 1
+    needs no communicator and touches no GPU."""
+
+    def __init__(self, rank, world, device, addr="127.0.0.1", port=29500):
+        self.L = load_library()
+        self.rank, self.world = int(rank), int(world)
+        h = ctypes.c_void_p()
+        check(self.L.tcmp_dist_init(self.rank, self.world, int(device), addr.encode(), int(port),
+                                    ctypes.byref(h)))
+        self.h = h
+
+    def barrier(self):
+        check(self.L.tcmp_dist_barrier(self.h))
+
+    def allreduce(self, values, op=REDUCE_SUM):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.float64).reshape(-1)).copy()
+        check(self.L.tcmp_dist_allreduce(self.h, _d(v), len(v), int(op)))
+        return v
+
+    def allgather_i64(self, values):
+        v = np.ascontiguousarray(np.asarray(values, dtype=np.int64).reshape(-1))
+        out = np.zeros(self.world * len(v), dtype=np.int64)
+        check(self.L.tcmp_dist_allgather_i64(self.h, v.ctypes.data_as(_i64p), len(v),
+                                             out.ctypes.data_as(_i64p)))
+        return out.reshape(self.world, len(v))
+
+    def gather_paths(self, ids, rows, data, cap_queries, cap_rows):
+        """tcmp_gather_paths: (ids, rows, data) on rank 0, None elsewhere."""
+        ids = np.ascontiguousarray(ids, dtype=np.int64)
+        rows = np.ascontiguousarray(rows, dtype=np.int64)
+        data = np.ascontiguousarray(data, dtype=np.float64).reshape(-1, TRAJ_COLS)
+        oi = np.zeros(max(cap_queries, 1), dtype=np.int64)
+        orows = np.zeros(max(cap_queries, 1), dtype=np.int64)
+        od = np.zeros((max(cap_rows, 1), TRAJ_COLS))
+        nq, nr = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(self.L.tcmp_gather_paths(self.h, len(ids), ids.ctypes.data_as(_i64p),
+                                       rows.ctypes.data_as(_i64p), _d(data), int(cap_queries),
+                                       int(cap_rows), oi.ctypes.data_as(_i64p),
+                                       orows.ctypes.data_as(_i64p), _d(od), ctypes.byref(nq),
+                                       ctypes.byref(nr)))
+        if self.rank != 0:
+            return None
+        return oi[:nq.value], orows[:nq.value], od[:nr.value]
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.tcmp_dist_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def rendezvous(rank, world, addr, port, blob, timeout_ms=60000):
+    """tcmp_rendezvous: rank 0's `blob` (bytes) to every rank; returns the received bytes."""
+    buf = ctypes.create_string_buffer(bytes(blob) if rank == 0 else b"\0" * len(blob), len(blob))
+    check(load_library().tcmp_rendezvous(int(rank), int(world), addr.encode(), int(port),
+                                         ctypes.cast(buf, ctypes.c_void_p), len(blob),
+                                         int(timeout_ms)))
+    return buf.raw
 
 
 _engines = {}

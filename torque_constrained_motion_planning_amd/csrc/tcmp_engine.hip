@@ -42,6 +42,15 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+}  // namespace
+
+// error channel shared with tcmp_dist.cpp (same thread-local message)
+namespace tcmp_err {
+int set(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace tcmp_err
+
+namespace {
+
 #define HIPCHK(x)                                                                      \
   do {                                                                                 \
     hipError_t e_ = (x);                                                               \
@@ -1106,6 +1115,12 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
   for (int i = 0; i < 24 && 12 + i < n; ++i) out[12 + i] = ex[i];
 #endif
+  return 0;
+}
+
+int tcmp_synchronize(tcmp_handle* h) {
+  if (int rc = set_dev(h)) return rc;
+  HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
 

@@ -1,14 +1,21 @@
 """rrt_star.py drop-in: force-aware RRT* with the reference's callback API.
 
-Reference: src/rrt_star.py:151-211.  When every callback was built by this package
-(utils.get_*_fn, panda_primitives torque tests / dynamics fn), the loop runs on the GPU
-engine: the host keeps the reference's RNG consumption (Python `random()` for the goal
-bias, np.random.uniform through the sample fn) and hands each iteration's draw to
-tcmp_plan_round (nearest / extend / collision / torque / insert / rewire on the device),
-then tcmp_plan_finish does retrace + min-jerk + the final dynamic torque validation.
-Foreign callbacks run the same algorithm on the host, calling them one at a time.
+Reference: src/rrt_star.py:151-211 (rrt_star_force_aware).  Three ways through it, picked by
+which callbacks this package built (utils.get_*_fn, panda_primitives torque tests / dynamics
+fn -- recognised by type):
 
-rrt_star_batched() is the engine-native frontier: B device-sampled candidates per round.
+* engine loop -- distance, extend, collision and torque are the package's own: the tree lives
+  on the GPU.  The host keeps the reference's RNG consumption (Python `random()` for the goal
+  bias, then the sample callback, which may be foreign) and hands each iteration's draw to
+  tcmp_plan_round (nearest / extend / collision / torque / insert / rewire on the device);
+  tcmp_plan_finish does retrace + min-jerk + the final dynamic torque validation.  A foreign
+  dynam_fn is applied on the host to the engine's retraced waypoints.
+* host loop -- distance or extend is foreign (or informed=True): the tree is kept as arrays
+  on the host (_Tree).  Each foreign callback is called exactly where the reference calls it;
+  the package's own collision / torque tests are evaluated by the engine in one batched
+  launch per extend sequence (tcmp_check_configs / tcmp_torque_ok, or tcmp_check_edges for
+  the whole edge when extend is native too), and a native distance is a vectorised argmin.
+* rrt_star_batched -- the engine-native frontier: B device-sampled candidates per round.
 """
 from __future__ import print_function
 
@@ -26,91 +33,13 @@ def elapsed_time(start_time):
     return time() - start_time
 
 
-def argmin(function, sequence):  # rrt_star.py:9-14
-    values = list(sequence)
-    scores = [function(x) for x in values]
-    return values[scores.index(min(scores))]
-
-
-class OptimalNode(object):  # rrt_star.py:18-63
-    def __init__(self, config, parent=None, d=0, path=[], iteration=None):
-        self.config = config
-        self.parent = parent
-        self.children = set()
-        self.d = d
-        self.path = path
-        if parent is not None:
-            self.cost = parent.cost + d
-            self.parent.children.add(self)
-        else:
-            self.cost = d
-        self.solution = False
-        self.creation = iteration
-        self.last_rewire = iteration
-
-    def set_solution(self, solution):
-        if self.solution is solution:
-            return
-        self.solution = solution
-        if self.parent is not None:
-            self.parent.set_solution(solution)
-
-    def retrace(self):
-        if self.parent is None:
-            return self.path + [self.config]
-        return self.parent.retrace() + self.path + [self.config]
-
-    def rewire(self, parent, d, path, iteration=None):
-        if self.solution:
-            self.parent.set_solution(False)
-        self.parent.children.remove(self)
-        self.parent = parent
-        self.parent.children.add(self)
-        if self.solution:
-            self.parent.set_solution(True)
-        self.d = d
-        self.path = path
-        self.update()
-        self.last_rewire = iteration
-
-    def update(self):
-        self.cost = self.parent.cost + self.d
-        for n in self.children:
-            n.update()
-
-
-def safe_path(sequence, collision):  # rrt_star.py:82-88
-    path = []
-    for q in sequence:
-        if collision(q):
-            break
-        path.append(q)
-    return path
-
-
-def safe_path_force_aware(sequence, collision, torque):  # rrt_star.py:90-98
-    path = []
-    for q in sequence:
-        if collision(q):
-            break
-        if not torque(q):
-            break
-        path.append(q)
-    return path
-
-
-def _native(distance, sample, extend, collision, torque_fn, dynam_fn):
+# ---- which callbacks are the package's own ---------------------------------------------------
+def _kinds(distance, sample, extend, collision, torque_fn, dynam_fn):
     from .panda_primitives import DynamFn, TorqueTest
-    from .utils import CollisionFn, DistanceFn, ExtendFn, SampleFn
-    return (isinstance(distance, DistanceFn) and isinstance(sample, SampleFn)
-            and isinstance(extend, ExtendFn) and isinstance(collision, CollisionFn)
-            and isinstance(torque_fn, TorqueTest) and isinstance(dynam_fn, DynamFn)
-            and np.allclose(sample.lower, _lib_limits()[0]) and np.allclose(sample.upper, _lib_limits()[1]))
-
-
-def _lib_limits():
-    from .scene import JOINT_LOWER, JOINT_UPPER
-    return JOINT_LOWER, JOINT_UPPER
+    from .utils import CollisionFn, DistanceFn, ExtendFn
+    return dict(distance=isinstance(distance, DistanceFn), extend=isinstance(extend, ExtendFn),
+                collision=isinstance(collision, CollisionFn),
+                torque=isinstance(torque_fn, TorqueTest), dynam=isinstance(dynam_fn, DynamFn))
 
 
 def _radius_value(radius):
@@ -120,11 +49,53 @@ def _radius_value(radius):
     return float(r[0])
 
 
-def _finish(eng, start_hint=None):
+def rrt_star_force_aware(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn,
+                         radius, max_time=INF, max_iterations=INF, goal_probability=.2,
+                         informed=False):
+    """rrt_star.py:151-211 -> (path, vels, accels, psg) or (None, None, None, None)."""
+    k = _kinds(distance, sample, extend, collision, torque_fn, dynam_fn)
+    if not informed and k["distance"] and k["extend"] and k["collision"] and k["torque"]:
+        res, _, _ = _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn,
+                                dynam_fn, radius, max_iterations, goal_probability, k["dynam"])
+        return res
+    return _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn,
+                     radius, max_time, max_iterations, goal_probability, informed, k)
+
+
+# ---- shared tail: dynam_fn + final validation (rrt_star.py:202-211) --------------------------
+def _validate_and_return(rrt_path, dynam_fn, torque_fn, native_torque):
+    path, psg, vels, accels = dynam_fn(rrt_path, len(rrt_path))
+    vels = vels[:len(path)]
+    accels = accels[:len(path)]
+    if path is None:
+        return None, None, None, None
+    if native_torque and len(path):
+        q = np.asarray(path, dtype=np.float64)[:, :7]
+        first_fail, _ = _lib.engine().validate(q, np.asarray(vels, dtype=np.float64)[:, :7],
+                                               np.asarray(accels, dtype=np.float64)[:, :7],
+                                               torque_fn.mode, torque_fn.payload_mass,
+                                               want_tau=False)
+        if first_fail >= 0:
+            return None, None, None, None
+    else:
+        for i in range(len(path)):
+            if not torque_fn(path[i], velocities=vels[i], accelerations=accels[i]):
+                return None, None, None, None
+    return path, vels, accels, psg
+
+
+def _finish(eng, dynam_fn=None, torque_fn=None):
+    """tcmp_plan_finish -> the reference's return tuple.  dynam_fn: a foreign dynamics fn,
+    applied on the host to the engine's retraced waypoints (else the engine's min-jerk and
+    validation stand)."""
     r = eng.plan_finish()
     if r.status == _lib.PLAN_NO_GOAL:
         print("failed to find goal")
         return (None, None, None, None), r, None
+    if dynam_fn is not None:
+        out = eng.plan_fetch(r)
+        rrt_path = [tuple(x) for x in out["waypoints"]]
+        return _validate_and_return(rrt_path, dynam_fn, torque_fn, True), r, out
     print("run min jerk")
     if r.status == _lib.PLAN_MINJERK_ASSERT:
         raise AssertionError("Invalid number of intervals chosen (must be greater than 0)")
@@ -138,20 +109,9 @@ def _finish(eng, start_hint=None):
     return (path, vels, accels, psg), r, out
 
 
-def rrt_star_force_aware(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn,
-                         radius, max_time=INF, max_iterations=INF, goal_probability=.2,
-                         informed=False):
-    """rrt_star.py:151-211 -> (path, vels, accels, psg) or (None, None, None, None)."""
-    if not informed and _native(distance, sample, extend, collision, torque_fn, dynam_fn):
-        res, _, _ = _rrt_native(start, goal, distance, sample, extend, collision, torque_fn,
-                                dynam_fn, radius, max_iterations, goal_probability)
-        return res
-    return _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn,
-                     radius, max_time, max_iterations, goal_probability, informed)
-
-
-def _rrt_native(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
-                max_iterations, goal_probability):
+# ---- engine loop ---------------------------------------------------------------------------
+def _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
+                max_iterations, goal_probability, native_dynam=True):
     if max_iterations == INF:
         raise ValueError("max_iterations must be finite (the reference's time guard never "
                          "fires, rrt_star.py:159, so INF iterations never return)")
@@ -160,7 +120,8 @@ def _rrt_native(start, goal, distance, sample, extend, collision, torque_fn, dyn
     start = tuple(float(x) for x in start)
     goal = tuple(float(x) for x in goal)
     st = eng.plan_begin(start, goal, torque_fn.mode, torque_fn.payload_mass,
-                        dynam_fn.execution_time, max_nodes=max_iterations + 1, max_batch=1,
+                        dynam_fn.execution_time if native_dynam else 5.0,
+                        max_nodes=max_iterations + 1, max_batch=1,
                         weights=distance.weights, resolutions=extend.resolutions,
                         radius=_radius_value(radius), goal_probability=goal_probability)
     if st == _lib.PLAN_START_GOAL_COLLISION:
@@ -169,11 +130,12 @@ def _rrt_native(start, goal, distance, sample, extend, collision, torque_fn, dyn
     goal_found = False
     it = 0
     while it < max_iterations:
+        # rrt_star.py:160-161: random() only while the goal is open and it > 0
         do_goal = (not goal_found) and (it == 0 or random() < goal_probability)
         s = goal if do_goal else sample()
         it += 1
-        goal_found = eng.plan_round(np.asarray([s], dtype=np.float64), [do_goal])
-    return _finish(eng)
+        goal_found = eng.plan_round(np.asarray([s], dtype=np.float64)[:, :7], [do_goal])
+    return _finish(eng, None if native_dynam else dynam_fn, torque_fn)
 
 
 def rrt_star_batched(start, goal, obstacles, torque_mode, payload_mass, execution_time,
@@ -198,52 +160,147 @@ def rrt_star_batched(start, goal, obstacles, torque_mode, payload_mass, executio
     return _finish(eng)
 
 
+# ---- host loop -------------------------------------------------------------------------------
+class _Tree:
+    """The reference's OptimalNode graph (rrt_star.py:18-63) as arrays.
+
+    Node i: the configuration object the callbacks produced, a row of `q` (float copy for the
+    vectorised nearest), the parent index (-1 for the root), the cost (parent cost + edge
+    length), and its edge's intermediate points (retrace output, rrt_star.py:42-45) -- either
+    a list, or (from, to, n_safe) when the engine checked the edge, regenerated through the
+    package's extend fn at retrace.  Children sets, set_solution and the recursive update()
+    are not kept: the force-aware loop only rewires the node it has just inserted, which has
+    no children yet (rrt_star.py:183-192; its second rewire loop never runs because the
+    `filter` iterator is already exhausted, rrt_star.py:193)."""
+
+    def __init__(self, root):
+        self.configs = [root]
+        self.q = np.zeros((1024, 7))
+        self.q[0] = np.asarray(root, dtype=np.float64)[:7]
+        self.parent = [-1]
+        self.cost = [0.0]
+        self.edge = [[]]
+
+    def __len__(self):
+        return len(self.configs)
+
+    def add(self, config, parent, d, edge):
+        n = len(self.configs)
+        if n == len(self.q):
+            self.q = np.concatenate([self.q, np.zeros_like(self.q)])
+        self.q[n] = np.asarray(config, dtype=np.float64)[:7]
+        self.configs.append(config)
+        self.parent.append(parent)
+        self.cost.append(self.cost[parent] + d)
+        self.edge.append(edge)
+        return n
+
+    def reparent(self, i, parent, d, edge):
+        self.parent[i] = parent
+        self.cost[i] = self.cost[parent] + d
+        self.edge[i] = edge
+
+    def retrace(self, i, extend):
+        chain = []
+        while i >= 0:
+            chain.append(i)
+            i = self.parent[i]
+        out = []
+        for n in reversed(chain):
+            e = self.edge[n]
+            if isinstance(e, tuple):  # engine-checked edge: regenerate its points
+                a, b, n_safe = e
+                pts = []
+                for k, q in enumerate(extend(a, b)):
+                    if k >= n_safe - 1:
+                        break
+                    pts.append(q)
+                e = pts
+            out.extend(e)
+            out.append(self.configs[n])
+        return out
+
+
 def _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
-              max_time=INF, max_iterations=INF, goal_probability=.2, informed=False):
-    """The reference loop verbatim (rrt_star.py:151-211) for foreign callbacks."""
+              max_time=INF, max_iterations=INF, goal_probability=.2, informed=False, kinds=None):
+    """rrt_star.py:151-211 with the tree on the host, for foreign distance / extend callbacks
+    (and informed=True).  Callback call order is the reference's, except that the package's
+    own collision and torque tests are evaluated for a whole extend sequence at once (they
+    are pure functions, so that is unobservable)."""
+    k = kinds if kinds is not None else _kinds(distance, sample, extend, collision, torque_fn,
+                                               dynam_fn)
+    eng = collision.engine if k["collision"] else None
     if collision(start) or collision(goal):
         print("start config in collision")
         return (None, None, None, None)
-    nodes = [OptimalNode(start)]
+    w = np.asarray(distance.weights, dtype=np.float64) if k["distance"] else None
+
+    def nearest(tree, s):
+        if w is not None:  # argmin (rrt_star.py:9-14): first index wins ties
+            d = tree.q[:len(tree)] - np.asarray(s, dtype=np.float64)[:7]
+            return int(np.argmin(np.sqrt((d * d) @ w)))
+        best, bi = INF, 0
+        for i, c in enumerate(tree.configs):
+            v = distance(c, s)
+            if v < best:
+                best, bi = v, i
+        return bi
+
+    def safe_prefix(a, b):
+        """safe_path_force_aware(extend(a, b), collision, torque) (rrt_star.py:90-98):
+        (last safe configuration or None, that edge's intermediate points)."""
+        if k["extend"] and k["collision"] and k["torque"]:
+            ns, _, last = eng.check_edges([a], [b], torque_fn.mode, torque_fn.payload_mass,
+                                          resolutions=extend.resolutions)
+            if ns[0] == 0:
+                return None, None
+            return tuple(last[0]), (a, b, int(ns[0]))
+        pts = list(extend(a, b))
+        coll = collision.batch(pts) if (k["collision"] and pts) else None
+        tq = (_lib.engine().torque_ok(np.asarray(pts, dtype=np.float64)[:, :7], torque_fn.mode,
+                                      torque_fn.payload_mass)
+              if (k["torque"] and pts) else None)
+        n = 0
+        for i, q in enumerate(pts):
+            if (coll[i] if coll is not None else collision(q)):
+                break
+            if not (tq[i] if tq is not None else torque_fn(q)):
+                break
+            n += 1
+        if n == 0:
+            return None, None
+        return pts[n - 1], pts[:n - 1]
+
+    tree = _Tree(start)
     goal_n = None
     t0 = time()
     it = 0
-    while (t0 - time()) < max_time and it < max_iterations:
+    while (t0 - time()) < max_time and it < max_iterations:  # (sic) rrt_star.py:159
         do_goal = goal_n is None and (it == 0 or random() < goal_probability)
         s = goal if do_goal else sample()
-        if informed and goal_n is not None and distance(start, s) + distance(s, goal) >= goal_n.cost:
+        if informed and goal_n is not None and \
+                distance(start, s) + distance(s, goal) >= tree.cost[goal_n]:
             print("greater than cost")
             continue
         it += 1
-        nearest = argmin(lambda n: distance(n.config, s), nodes)
-        path = safe_path_force_aware(extend(nearest.config, s), collision, torque_fn)
-        if len(path) == 0:
+        near = nearest(tree, s)
+        last, edge = safe_prefix(tree.configs[near], s)
+        if last is None:
             continue
-        new = OptimalNode(path[-1], parent=nearest, d=distance(nearest.config, path[-1]),
-                          path=path[:-1], iteration=it)
-        if do_goal and distance(new.config, goal) < 1e-2:
+        new = tree.add(last, near, distance(tree.configs[near], last), edge)
+        if do_goal and distance(last, goal) < 1e-2:
             goal_n = new
-            goal_n.set_solution(True)
-        neighbors = filter(lambda n: distance(n.config, new.config) < radius, nodes)
-        nodes.append(new)
-        for n in neighbors:
-            d = distance(n.config, new.config)
-            if n.cost + d < new.cost:
-                path = safe_path_force_aware(extend(n.config, new.config), collision, torque_fn)
-                if len(path) != 0 and distance(new.config, path[-1]) < 1e-6:
-                    new.rewire(n, d, path[:-1], iteration=it)
-        # the reference's second rewire loop never runs: `neighbors` is an exhausted
-        # iterator by then (rrt_star.py:193)
+        # neighbours within `radius` among all nodes, `new` included (the lazy filter is
+        # consumed after nodes.append(new), rrt_star.py:183-186), in index order
+        for n in range(len(tree)):
+            if not distance(tree.configs[n], last) < radius:
+                continue
+            d = distance(tree.configs[n], last)
+            if tree.cost[n] + d < tree.cost[new]:
+                end, pts = safe_prefix(tree.configs[n], last)
+                if end is not None and distance(last, end) < 1e-6:
+                    tree.reparent(new, n, d, pts)
     if goal_n is None:
         print("failed to find goal")
         return None, None, None, None
-    rrtPath = goal_n.retrace()
-    path, psg, vels, accels = dynam_fn(rrtPath, len(rrtPath))
-    vels = vels[:len(path)]
-    accels = accels[:len(path)]
-    if path is None:
-        return None, None, None, None
-    for i in range(len(path)):
-        if not torque_fn(path[i], velocities=vels[i], accelerations=accels[i]):
-            return None, None, None, None
-    return path, vels, accels, psg
+    return _validate_and_return(tree.retrace(goal_n, extend), dynam_fn, torque_fn, k["torque"])

@@ -109,7 +109,7 @@ def get_mass(body):
 def obstacle_array(fixed):
     """Pack the boxes of Problem.fixed into the (n, 15) C-ABI layout (convex meshes are
     packed separately by mesh_pack)."""
-    if fixed is None:
+    if fixed is None or isinstance(fixed, MeshPack):
         fixed = []
     if isinstance(fixed, np.ndarray):
         if fixed.size == 0:

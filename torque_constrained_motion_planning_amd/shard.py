@@ -1,14 +1,18 @@
 """Multi-GPU query sharding: independent planning queries are dealt round-robin
-to ranks (one process per GPU); each rank plans its queries with its own engine, and the
-solved trajectories are gathered to rank 0 -- the only collective on the path (RCCL over
-xGMI with the nccl backend, gloo in the CPU tests).
+to ranks (one process per GPU); each rank plans its queries with its own engines, and the
+solved trajectories are gathered to rank 0 -- the only collective on the path, RCCL over
+xGMI inside libtcmp.so (tcmp_gather_paths; no PyTorch).
 
 Trajectory record per query: rows of [q(7), qd(7), qdd(7), dt(1)] (Conf values,
 velocities, accelerations, dt of create_trajectory, utils.py:3340-3347), float64.
 """
+import os
+
 import numpy as np
 
-TRAJ_COLS = 22
+from . import _lib
+
+TRAJ_COLS = _lib.TRAJ_COLS
 
 
 def queries_for_rank(n_queries, world, rank):
@@ -29,42 +33,43 @@ def unpack_trajectory(a):
     return {"q": a[:, 0:7], "qd": a[:, 7:14], "qdd": a[:, 14:21], "psg": a[:, 21]}
 
 
-def gather_trajectories(dist, trajs, query_ids, world, rank, device="cpu"):
-    """Gather every rank's list of (query_id, (K,22) array) to rank 0.
+def pack_paths(trajs, query_ids):
+    """Local paths -> the wire form of tcmp_gather_paths: (ids, rows, data)."""
+    ids = np.asarray(list(query_ids), dtype=np.int64)
+    rows = np.asarray([len(t) for t in trajs], dtype=np.int64)
+    data = (np.concatenate([np.asarray(t, dtype=np.float64).reshape(-1, TRAJ_COLS) for t in trajs])
+            if len(trajs) else np.zeros((0, TRAJ_COLS)))
+    return ids, rows, data
 
-    One size exchange (all_gather of counts) and one padded gather of a single buffer per
-    rank.  Returns {query_id: (K,22) array} on rank 0, None elsewhere."""
-    import torch
-    # header: per local query (id, rows)
-    n_local = len(trajs)
-    counts = torch.tensor([n_local, sum(len(t) for t in trajs)], dtype=torch.int64, device=device)
-    all_counts = [torch.zeros_like(counts) for _ in range(world)]
-    dist.all_gather(all_counts, counts)
-    max_q = max(int(c[0]) for c in all_counts)
-    max_rows = max(int(c[1]) for c in all_counts)
-    hdr = torch.full((max(max_q, 1), 2), -1, dtype=torch.int64, device=device)
-    body = torch.zeros((max(max_rows, 1), TRAJ_COLS), dtype=torch.float64, device=device)
-    r = 0
-    for i, (qid, t) in enumerate(zip(query_ids, trajs)):
-        hdr[i, 0] = int(qid)
-        hdr[i, 1] = len(t)
-        if len(t):
-            body[r:r + len(t)] = torch.from_numpy(np.asarray(t, dtype=np.float64)).to(device)
-        r += len(t)
-    hdrs = [torch.zeros_like(hdr) for _ in range(world)] if rank == 0 else None
-    bodies = [torch.zeros_like(body) for _ in range(world)] if rank == 0 else None
-    dist.gather(hdr, hdrs, dst=0)
-    dist.gather(body, bodies, dst=0)
-    if rank != 0:
+
+def unpack_paths(ids, rows, data):
+    """(ids, rows, data) -> {query id: (K, 22) rows}."""
+    out, r = {}, 0
+    for q, k in zip(ids, rows):
+        out[int(q)] = np.asarray(data[r:r + k]).copy()
+        r += int(k)
+    return out
+
+
+def comm_from_env(device=None):
+    """The job's communicator from the launcher's environment (torchrun / torch.distributed.run
+    set RANK, WORLD_SIZE, LOCAL_RANK, MASTER_ADDR, MASTER_PORT).  The rendezvous of rank 0's
+    RCCL id uses MASTER_PORT + 1 (the launcher's own store holds MASTER_PORT) unless
+    TCMP_RDZV_PORT is set."""
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    addr = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    port = int(os.environ.get("TCMP_RDZV_PORT", int(os.environ.get("MASTER_PORT", "29500")) + 1))
+    return _lib.Comm(rank, world, local if device is None else device, addr, port)
+
+
+def gather_trajectories(comm, trajs, query_ids):
+    """Gather every rank's list of (K, 22) paths to rank 0 (tcmp_gather_paths over RCCL).
+    Returns {query_id: (K, 22) array} on rank 0, None elsewhere."""
+    ids, rows, data = pack_paths(trajs, query_ids)
+    sizes = comm.allgather_i64([len(ids), int(rows.sum())])
+    got = comm.gather_paths(ids, rows, data, int(sizes[:, 0].sum()), int(sizes[:, 1].sum()))
+    if got is None:
         return None
-    result = {}
-    for h, b in zip(hdrs, bodies):
-        h = h.cpu().numpy()
-        b = b.cpu().numpy()
-        r = 0
-        for qid, k in h:
-            if qid < 0:
-                continue
-            result[int(qid)] = b[r:r + k].copy()
-            r += k
-    return result
+    return unpack_paths(*got)

@@ -162,7 +162,8 @@ class CollisionFn:
     """get_collision_fn (utils.py:3165-3218): joint limits, the self-collision link pairs when
     self_collisions (get_self_link_pairs, utils.py:3138-3149), then every moving link hull vs
     every fixed obstacle with the -MAX_DISTANCE closest-point threshold.  Evaluated by the
-    engine (tcmp_check_configs)."""
+    engine (tcmp_check_configs) on a handle of its own, created on first use with the scene
+    uploaded once; rrt_star_force_aware plans on that same handle."""
 
     def __init__(self, body, obstacles, device=0, self_collisions=False):
         self.body = body
@@ -170,19 +171,22 @@ class CollisionFn:
         self.meshes = mesh_pack(obstacles)
         self.device = device
         self.self_collisions = bool(self_collisions)
+        self._engine = None
 
     @property
     def engine(self):
-        e = _lib.engine(self.device)
-        e.set_scene(self.obstacles, self.meshes)
-        e.set_self_collision(self.self_collisions)
-        return e
+        if self._engine is None:
+            e = _lib.Engine(self.device)
+            e.set_scene(self.obstacles, self.meshes)
+            e.set_self_collision(self.self_collisions)
+            self._engine = e
+        return self._engine
 
     def __call__(self, q, verbose=False):
-        return bool(self.engine.collides([q])[0])
+        return bool(self.engine.collides([np.asarray(q, dtype=np.float64)[:7]])[0])
 
     def batch(self, qs):
-        return self.engine.collides(qs)
+        return self.engine.collides(np.asarray(qs, dtype=np.float64)[:, :7])
 
 
 def get_collision_fn(body, joints, obstacles=[], attachments=[], self_collisions=True,
