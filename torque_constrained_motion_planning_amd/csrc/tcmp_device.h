@@ -1011,11 +1011,13 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 
 // MESH = false: a scene without convex meshes (tcmp_set_meshes count 0) -- the mesh tiers
 // are compiled out, which keeps the box-only kernels' register allocation unchanged.
+// The joint-limit test (inclusive, utils.py:3181-3182) is the caller's: `active` lanes are
+// those within the limits that still need their obstacle (and self) pairs.
 template <bool MESH>
-__device__ __forceinline__ bool collides_wave(const double q[7], const double cq[7],
-                                              const double sq[7], bool active,
-                                              const Scene sc, const Geo g, StepStats& st) {
-  bool coll = active && limits_violated(q);
+__device__ __forceinline__ bool collides_wave(const double cq[7], const double sq[7],
+                                              bool active, const Scene sc, const Geo g,
+                                              StepStats& st) {
+  bool coll = false;
   if (sc.n_obs == 0 && !(MESH && sc.self_coll)) return coll;
   const int lane = lane_id();
   unsigned* queue = sc.wq;

@@ -206,6 +206,7 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
 
 #include "tcmp_nn.h"
 #include "tcmp_nn32.h"
+#include "tcmp_nng.h"
 #include "tcmp_insert.h"
 #include "tcmp_ik.h"
 
@@ -239,11 +240,11 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
   const int lane = lane_id();
   int e = -1, i = 0, n = 0;
   bool done = false;
-  double q[7], q2[7];
+  double q[7];  // last safe configuration of the lane's edge (the target is re-read per step)
 #pragma unroll
-  for (int k = 0; k < 7; ++k) { q[k] = 0.5 * (kLo[k] + kHi[k]); q2[k] = q[k]; }
+  for (int k = 0; k < 7; ++k) q[k] = 0.5 * (kLo[k] + kHi[k]);
   StepStats ss = {};
-  unsigned long long steps = 0;
+  unsigned steps = 0;  // this lane's extend steps (32-bit: one register)
 #ifdef TCMP_PROF
   unsigned long long c_total = 0, c_fetch = 0, c_coll = 0, c_torque = 0, c_tail = 0, c_sincos = 0;
   const unsigned long long c_start = clock64();
@@ -267,6 +268,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
         if (my < J.n) {
           e = J.order ? J.order[my] : my;
           const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
+          double q2[7];
           load7(J.from_base + 8 * src, q);
           load7(J.to + 8 * (size_t)e, q2);
           n = num_steps(q, q2, res);
@@ -281,34 +283,50 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     { const unsigned long long c1 = clock64(); c_fetch += c1 - c0; c0 = c1; }
 #endif
     const bool active = e >= 0;
-    double qn[7];
-#pragma unroll
-    for (int k = 0; k < 7; ++k) qn[k] = q[k];
-    if (active) refine_step(qn, q2, n, i);
+    // The step's configuration qn, its sin/cos and the torque test come first; during the
+    // collision check only q (the last safe configuration) and cq/sq stay live -- the target
+    // q2 is re-read from memory and qn regenerated (the same arithmetic, so the same bits)
+    // afterwards, which keeps the check's register peak below the spill point.
+    bool tok = true, lim = false;
     double cq[7], sq[7];
+    {
+      double qn[7], q2[7];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
+      for (int k = 0; k < 7; ++k) qn[k] = q[k];
+      if (active) {
+        load7(J.to + 8 * (size_t)e, q2);
+        refine_step(qn, q2, n, i);
+      }
+#pragma unroll
+      for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
+      lim = active && limits_violated(qn);
+    }
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_sincos += c1 - c0; c0 = c1; }
 #endif
-    const bool coll = collides_wave<MESH>(qn, cq, sq, active, sc, g, ss);
-#ifdef TCMP_PROF
-    { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
-#endif
-    bool ok = active && !coll;
-    if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
+    // torque test (panda_primitives.py:155-193) -- independent of the collision result, so
+    // its order against the collision check does not matter (rrt_star.py:93-96)
+    if (active && !lim && P.torque_mode != TCMP_TORQUE_BASE) {
       const double z[7] = {0, 0, 0, 0, 0, 0, 0};
-      ok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
-                                            : torque_ok<false>(cq, sq, z, z, P.mass);
+      tok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
+                                             : torque_ok<false>(cq, sq, z, z, P.mass);
     }
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_torque += c1 - c0; c0 = c1; }
 #endif
+    // lanes already failing (limits or torque) need no obstacle pairs
+    // every lane calls it (wave-cooperative); lanes already failing only ride along
+    const bool coll = collides_wave<MESH>(cq, sq, active && !lim && tok, sc, g, ss) || lim;
+#ifdef TCMP_PROF
+    { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
+#endif
+    const bool ok = active && !coll && tok;
     if (active) {
       ++steps;
       if (ok) {
-#pragma unroll
-        for (int k = 0; k < 7; ++k) q[k] = qn[k];
+        double q2[7];
+        load7(J.to + 8 * (size_t)e, q2);
+        refine_step(q, q2, n, i);
         ++i;
       }
       if (!ok || i == n) {
@@ -322,7 +340,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
     c_tail += clock64() - c0;
 #endif
   }
-  const unsigned long long a = wave_sum_u64(steps), b = wave_sum_u64(ss.pairs_tested),
+  const unsigned long long a = wave_sum_u64((unsigned long long)steps), b = wave_sum_u64(ss.pairs_tested),
                            c = wave_sum_u64(ss.pairs_sat), d = wave_sum_u64(ss.pairs_exact);
   if (lane == 0) {
     atomicAdd(&st->edge_steps, a);
@@ -457,7 +475,8 @@ __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st
       if (alive) refine_step(qq, qn, ns, i);
       double cq[7], sq[7];
       for (int k = 0; k < 7; ++k) sincos(qq[k], &sq[k], &cq[k]);
-      const bool coll = collides_wave<MESH>(qq, cq, sq, alive, sc, g, ss);
+      const bool lim = alive && limits_violated(qq);
+      const bool coll = collides_wave<MESH>(cq, sq, alive && !lim, sc, g, ss) || lim;
       bool ok = alive && !coll;
       if (ok && P.torque_mode != TCMP_TORQUE_BASE) {
         const double z[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -672,7 +691,8 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
   double cq[7], sq[7];
   for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
   StepStats ss = {0, 0, 0};
-  const bool c = collides_wave<MESH>(x, cq, sq, act, sc, g, ss);
+  const bool lim = act && limits_violated(x);
+  const bool c = collides_wave<MESH>(cq, sq, act && !lim, sc, g, ss) || lim;
   if (act) collides[i] = c ? 1 : 0;
 }
 
@@ -818,6 +838,7 @@ struct tcmp_handle {
   DBuf<unsigned long long> ckey;
   DBuf<unsigned char> sort_tmp;
   DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
+  int nn_mode = 0;            // nearest scan: 0 k_nearest_wave32 (depth-first), 1 k_nearest_bfs
   int nn_waves_per_cu = 16;
   DBuf<double> second;
   DBuf<long long> chain;
@@ -977,9 +998,8 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const doub
                                              kKeyBits + 1, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, st,
-                     cfg, h->svals.p, h->stree.p, h->stree32.p);
+                     cfg, h->svals.p, h->stree.p, h->stree32.p, T_bound, h->cflag.p, h->sflag.p);
   HIPCHK(hipGetLastError());
-  HIPCHK(hipMemsetAsync(h->cflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
   hipLaunchKernelGGL(k_nn_cut<kNnC>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
                      &st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
   HIPCHK(hipGetLastError());
@@ -990,12 +1010,13 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const doub
                      &st->n_nodes, (const int*)nullptr, h->cflag.p, h->cid.p, h->cstart.p,
                      &st->nn_cells);
   HIPCHK(hipGetLastError());
-  // one wave per cell; the cell count is device-side, so cover the worst case (one per node)
-  hipLaunchKernelGGL(k_nn_cell_boxes, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0, h->stream,
+  // one wave per cell, grid-stride: the cell count is device-side
+  const unsigned idx_grid = (unsigned)std::min<long long>(grid_for(T_bound * 64, 256),
+                                                          (long long)h->cu_count * 8);
+  hipLaunchKernelGGL(k_nn_cell_boxes, dim3(idx_grid), dim3(256), 0, h->stream,
                      st, h->stree.p, h->cstart.p, h->skeys.p, h->cboxf.p, h->ckey.p);
   HIPCHK(hipGetLastError());
   // super-cells: the same radix-tree cut over the cells' first keys
-  HIPCHK(hipMemsetAsync(h->sflag.p, 0, sizeof(int) * (size_t)T_bound, h->stream));
   hipLaunchKernelGGL(k_nn_cut<kNnS>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
                      (const long long*)nullptr, &st->nn_cells, h->ckey.p, h->sflag.p);
   HIPCHK(hipGetLastError());
@@ -1006,32 +1027,42 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const doub
                      (const long long*)nullptr, &st->nn_cells, h->sflag.p, h->sid.p,
                      h->sstart.p, &st->nn_supers);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_nn_build_supers, dim3(grid_for(T_bound * 64, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(k_nn_build_supers, dim3(idx_grid), dim3(256), 0,
                      h->stream, st, h->sstart.p, h->cboxf.p, h->sboxf.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(k_nn_build_blocks, dim3(grid_for(T_bound + 128, 256)), dim3(256), 0,
+  hipLaunchKernelGGL(k_nn_build_blocks, dim3(std::min<unsigned>(grid_for(T_bound + 128, 256), 1024)), dim3(256), 0,
                      h->stream, st, h->sboxf.p, h->bboxf.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, cand, nb,
                      h->ckeys_in.p, h->cvals_in.p);
   HIPCHK(hipGetLastError());
   // candidates only need locality (the scan order never changes a result): top 16 key bits
+  // for the one-candidate scan, the full key when a wave scans Morton-adjacent groups
   tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                              h->cvals_in.p, h->cperm.p, (size_t)nb,
-                                             kKeyBits + 1 - 16, kKeyBits + 1, h->stream));
+                                             kKeyBits + 1 - 16, kKeyBits + 1,
+                                             h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
                      h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
-  // one wave per candidate at a time; contiguous Morton-sorted runs per wave
-  HIPCHK(hipMemsetAsync(&st->nn_counter, 0, sizeof(int), h->stream));
-  HIPCHK(hipMemsetAsync(st->nn_queue, 0, sizeof(int) * 8, h->stream));
+  // one wave per candidate at a time; contiguous Morton-sorted runs per wave (k_nn_home
+  // cleared the queues)
   const long long waves = std::min<long long>(nb, (long long)h->cu_count * h->nn_waves_per_cu);
   const int per_wave = (int)((nb + waves - 1) / waves);
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
   h->mark_begin(F_NNSCAN, &e0);
-  if (P.uniform_w)
+  if (h->nn_mode == 1) {
+    if (P.uniform_w)
+      hipLaunchKernelGGL(k_nearest_bfs<true>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+                         h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,
+                         h->cperm.p, h->chome.p, nb, nn, second, score);
+    else
+      hipLaunchKernelGGL(k_nearest_bfs<false>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+                         h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,
+                         h->cperm.p, h->chome.p, nb, nn, second, score);
+  } else if (P.uniform_w)
     hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, st,
                        h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
                        h->chome.p, nb, nn, second, score);
@@ -1060,14 +1091,16 @@ __global__ void k_edge_order_keys(PlanParams P, const double* cfg, const int* nn
   vals[e] = e;
 }
 
-int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P) {
+// reset_counter = false: the plan's k_nn_home already cleared the work counter
+int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P, bool reset_counter = true) {
   if (J.n <= 0) return 0;
-  HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
-  // persistent grid: ~2 edges per lane keeps refill useful; bounded by residency
-  long long lanes = std::max<long long>(64, (J.n + 1) / 2);
-  long long blocks = (lanes + 255) / 256;
-  // resident blocks: 256-thread blocks hold one wave per SIMD each
+  if (reset_counter) HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
+  // persistent grid bounded by residency (256-thread blocks hold one wave per SIMD each).
+  // Above it, lanes refill from the longest-first queue; below it, one edge per lane --
+  // halving the lanes of a small round (65,536 edges) would leave half the chip idle.
   const long long cap = (long long)h->cu_count * std::max(2, TCMP_EDGE_MINW);
+  long long lanes = std::max<long long>(64, J.n);
+  long long blocks = (lanes + 255) / 256;
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
@@ -1210,6 +1243,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMalloc(&h->st_nn, sizeof(DevState)));
   HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
+  if (const char* e = getenv("TCMP_NN_MODE")) h->nn_mode = atoi(e);
   *out = h;
   return 0;
 }
@@ -1984,7 +2018,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
                                                h->stream));
     J.order = h->cperm.p;
   }
-  if (int rc = launch_edges(h, J, P)) return rc;
+  if (int rc = launch_edges(h, J, P, false)) return rc;
   h->mark_end(F_EDGES, e0);
   h->mark_begin(F_INSERT, &e0);
   {

@@ -24,9 +24,14 @@ constexpr int kNnS = 64;              // cells per super-cell
 
 __global__ __launch_bounds__(256) void k_nn_rows(DevState* st, const double* cfg,
                                                  const int* svals, double* stree,
-                                                 float* stree32) {
+                                                 float* stree32, long long T_bound, int* cflag,
+                                                 int* sflag) {
   const long long T = st->n_nodes;
   const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= T_bound) return;
+  // the cut kernels only set flags: clear both flag arrays here (no memset launches)
+  cflag[p] = 0;
+  sflag[p] = 0;
   if (p >= T) return;
   double q[7];
   const int n = svals[p];
@@ -100,8 +105,9 @@ __global__ __launch_bounds__(256) void k_nn_cell_boxes(DevState* st, const doubl
                                                        const unsigned long long* skeys,
                                                        float* cbox, unsigned long long* ckey) {
   const int C = st->nn_cells;
-  const long long c = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6;
-  if (c >= C) return;  // wave-uniform
+  // grid-stride over cells, one wave per cell (the count is device-side)
+  for (long long c = ((long long)blockIdx.x * 256 + threadIdx.x) >> 6; c < C;
+       c += ((long long)gridDim.x * 256) >> 6) {
   const int a = cstart[c], b = cstart[c + 1];
   const long long p = a + lane_id();
   double lo[7], hi[7];
@@ -130,6 +136,7 @@ __global__ __launch_bounds__(256) void k_nn_cell_boxes(DevState* st, const doubl
     bx[15] = __int_as_float(b - a);
     ckey[c] = skeys[a];
   }
+  }
 }
 
 // one wave per super-cell (a radix-tree subtree of <= kNnS cells): union of its cells' bounds;
@@ -137,8 +144,8 @@ __global__ __launch_bounds__(256) void k_nn_cell_boxes(DevState* st, const doubl
 __global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const int* sstart,
                                                          const float* cbox, float* sbox) {
   const int nsup = st->nn_supers;
-  const long long sw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (sw >= nsup) return;  // wave-uniform
+  for (long long sw = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; sw < nsup;
+       sw += ((long long)gridDim.x * blockDim.x) >> 6) {
   const int c0 = sstart[sw], c1 = sstart[sw + 1];
   const long long c = c0 + lane_id();
   float lo[7], hi[7];
@@ -161,6 +168,7 @@ __global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const int
     sbox[16 * sw + 7] = __int_as_float(c0);
     sbox[16 * sw + 15] = __int_as_float(c1 - c0);
   }
+  }
 }
 
 // blocks of 64 consecutive super-cells (Morton order): their f32 bounds, one wave per block,
@@ -168,8 +176,8 @@ __global__ __launch_bounds__(256) void k_nn_build_supers(DevState* st, const int
 __global__ __launch_bounds__(256) void k_nn_build_blocks(DevState* st, const float* sbox,
                                                          float* bbox) {
   const int nsup = st->nn_supers;
-  const long long b = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  if (b * 64 >= nsup) return;  // wave-uniform
+  for (long long b = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; b * 64 < nsup;
+       b += ((long long)gridDim.x * blockDim.x) >> 6) {
   const long long sp = b * 64 + lane_id();
   float lo[7], hi[7];
 #pragma unroll
@@ -191,6 +199,7 @@ __global__ __launch_bounds__(256) void k_nn_build_blocks(DevState* st, const flo
     bbox[16 * b + 7] = 0.f;
     bbox[16 * b + 15] = 0.f;
   }
+  }
 }
 
 // home cell of each Morton-sorted candidate: the cell holding its key's lower bound, and its
@@ -199,6 +208,11 @@ __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
                           const unsigned long long* ckeys, const int* cid, const int* sid, int nb,
                           int* home) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < 8) st->nn_queue[j] = 0;  // the scan's per-XCD queues (next launch)
+  if (j == 0) {
+    st->nn_counter = 0;
+    st->work_counter = 0;          // k_edges' lane-refill counter (launched after the scan)
+  }
   if (j >= nb) return;
   const long long T = st->n_nodes;
   const unsigned long long k = ckeys[j];

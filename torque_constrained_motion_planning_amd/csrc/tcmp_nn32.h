@@ -24,6 +24,7 @@
 #pragma once
 
 constexpr double kNnU32 = 5.9604644775390625e-08;  // 2^-24
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 constexpr double kNnG = 16.0 * kNnU32;
 
 __device__ __forceinline__ unsigned xcc_id() {
@@ -175,19 +176,28 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
         b2 = fmin(b2, dd);
       }
     };
+    // packed fp32 (v_pk_add / v_pk_fma: two joints per instruction); any association of the
+    // seven terms stays inside the error model's g = 16 u
+    const f32x2 s01 = {s32[0], s32[1]}, s23 = {s32[2], s32[3]}, s45 = {s32[4], s32[5]},
+                s6 = {s32[6], 0.f};
+    const f32x2 w01 = {w32[0], w32[1]}, w23 = {w32[2], w32[3]}, w45 = {w32[4], w32[5]},
+                w6 = {w32[6], 0.f};
     auto upd = [&](const float4 a, const float4 b, long long n) {
-      const float d0 = s32[0] - a.x, d1 = s32[1] - a.y, d2 = s32[2] - a.z, d3 = s32[3] - a.w,
-                  d4 = s32[4] - b.x, d5 = s32[5] - b.y, d6 = s32[6] - b.z;
-      float r;
+      const f32x2 d01 = s01 - f32x2{a.x, a.y}, d23 = s23 - f32x2{a.z, a.w},
+                  d45 = s45 - f32x2{b.x, b.y}, d6 = s6 - f32x2{b.z, 0.f};
+      f32x2 acc;
       if (UW) {
-        r = d0 * d0;
-        r = fmaf(d1, d1, r); r = fmaf(d2, d2, r); r = fmaf(d3, d3, r);
-        r = fmaf(d4, d4, r); r = fmaf(d5, d5, r); r = fmaf(d6, d6, r);
+        acc = d01 * d01;
+        acc = __builtin_elementwise_fma(d23, d23, acc);
+        acc = __builtin_elementwise_fma(d45, d45, acc);
+        acc = __builtin_elementwise_fma(d6, d6, acc);
       } else {
-        r = w32[0] * (d0 * d0);
-        r = fmaf(w32[1] * d1, d1, r); r = fmaf(w32[2] * d2, d2, r); r = fmaf(w32[3] * d3, d3, r);
-        r = fmaf(w32[4] * d4, d4, r); r = fmaf(w32[5] * d5, d5, r); r = fmaf(w32[6] * d6, d6, r);
+        acc = (w01 * d01) * d01;
+        acc = __builtin_elementwise_fma(w23 * d23, d23, acc);
+        acc = __builtin_elementwise_fma(w45 * d45, d45, acc);
+        acc = __builtin_elementwise_fma(w6 * d6, d6, acc);
       }
+      const float r = acc.x + acc.y;
       if (r <= Rf) refine(n);
       else r2 = fminf(r2, r);
     };
@@ -209,13 +219,16 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams
       bool val[4];
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        const long long n = (long long)cs[u] + lane;
-        val[u] = lane < cn[u];
+        // wave-uniform row base + lane offset: scalar-base loads, no per-lane 64-bit math
+        const int c0 = __builtin_amdgcn_readfirstlane(cs[u]);
+        const int cnt = __builtin_amdgcn_readfirstlane(cn[u]);
+        const float4* rp = reinterpret_cast<const float4*>(stree32) + 2 * (unsigned)c0;
+        val[u] = lane < cnt;
         if (val[u]) {
-          A[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n);
-          Bq[u] = *reinterpret_cast<const float4*>(stree32 + 8 * n + 4);
+          A[u] = rp[2 * lane];
+          Bq[u] = rp[2 * lane + 1];
         }
-        pairs += (unsigned long long)cn[u];
+        pairs += (unsigned long long)cnt;
       }
 #pragma unroll
       for (int u = 0; u < 4; ++u)
