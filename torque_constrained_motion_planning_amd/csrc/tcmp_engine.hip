@@ -122,8 +122,9 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
 // ------------------------------------------------------------------------------------------
 // k_sample: uniform configurations (utils.py:2941-2990 convex_combination of the limits)
 // ------------------------------------------------------------------------------------------
-__global__ void k_sample(PlanParams P, DevState* st, long long base, int nb, double* cand,
+__global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long long base, int nb, double* cand,
                          unsigned char* cgoal) {
+  const PlanParams P = *Pd;
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
   const long long it = base + j;
@@ -142,7 +143,8 @@ __global__ void k_sample(PlanParams P, DevState* st, long long base, int nb, dou
 // ------------------------------------------------------------------------------------------
 // k_goal_fix: the round's goal-biased lane takes the goal configuration (rrt_star.py:160-161)
 // ------------------------------------------------------------------------------------------
-__global__ void k_goal_fix(PlanParams P, DevState* st, double* cand, unsigned char* cgoal, int nb) {
+__global__ void k_goal_fix(const PlanParams* __restrict__ Pd, DevState* st, double* cand, unsigned char* cgoal, int nb) {
+  const PlanParams P = *Pd;
   const int j = st->round_goal;
   if (threadIdx.x == 0 && j < nb) {
 #pragma unroll
@@ -206,7 +208,6 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
 
 #include "tcmp_nn.h"
 #include "tcmp_nn32.h"
-#include "tcmp_nng.h"
 #include "tcmp_insert.h"
 #include "tcmp_ik.h"
 
@@ -231,8 +232,9 @@ struct EdgeJob {
 #define TCMP_EDGE_MINW 2  // min waves per SIMD the register allocation must allow
 #endif
 template <bool MESH>
-__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanParams P, Scene sc_g, Geo g_g,
+__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const PlanParams* __restrict__ Pd, Scene sc_g, Geo g_g,
                                                DevState* st) {
+  const PlanParams P = *Pd;
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
@@ -365,8 +367,9 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, PlanPa
 // rewire (rrt_star.py:183-192): neighbours of each new node within `radius` among the
 // round's snapshot, visited in index order; reparent when cheaper and the edge is safe.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st, Tree tr,
+__global__ __launch_bounds__(256) void k_rewire_scan(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
                                                      const int* rwlist, int* nbr, int* ncount) {
+  const PlanParams P = *Pd;
   // neighbours within `radius` of each flagged new node among the snapshot, in index order
   // (the order rrt_star.py:187 visits them); the snapshot streams through LDS tiles
   __shared__ double4 tile[2 * kNnTile];
@@ -410,9 +413,10 @@ __global__ __launch_bounds__(256) void k_rewire_scan(PlanParams P, DevState* st,
 }
 
 template <bool MESH>
-__global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st, Tree tr,
+__global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
                                                       const int* rwlist, const int* nbr,
                                                       const int* ncount, Scene sc_g, Geo g_g) {
+  const PlanParams P = *Pd;
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
@@ -511,8 +515,9 @@ __global__ __launch_bounds__(256) void k_rewire_apply(PlanParams P, DevState* st
 // retrace (rrt_star.py:42-45, 202): [start] + for each edge root->goal the first n_safe-1
 // regenerated extend points + the node's configuration.  One block.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_retrace(PlanParams P, DevState* st, Tree tr,
+__global__ __launch_bounds__(256) void k_retrace(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
                                                  long long* chain, double* wp, long long wp_cap) {
+  const PlanParams P = *Pd;
   __shared__ long long sL;
   __shared__ long long part[256];
   const int tid = threadIdx.x;
@@ -638,9 +643,10 @@ __device__ __forceinline__ bool torque_test_sample(int mode, double mass, const 
 }
 
 // dynam_fn + final validation + Conf.torques for the planner's path (grid-stride)
-__global__ __launch_bounds__(256) void k_traj(PlanParams P, DevState* st, const double* wp,
+__global__ __launch_bounds__(256) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
                                               double* oq, double* oqd, double* oqdd,
                                               double* opsg, double* otau) {
+  const PlanParams P = *Pd;
   if (st->status != 0 && st->status != TCMP_PLAN_VALIDATION_FAILED) return;
   const long long K = st->K, ni = st->ni, W = st->W;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < K;
@@ -780,6 +786,20 @@ enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_NNSCAN, F_COU
 struct EventPair {
   hipEvent_t a, b;
   int fam;
+  bool owned = false;  // recorded by a cached round graph's event nodes (not pool events)
+};
+
+// A captured sequence of device-sampled rounds (tcmp_plan_run) -- replayed with one
+// hipGraphLaunch instead of ~45 launches per round.  Kernels read the plan parameters and
+// state from device memory, so a graph serves every query of the same shape; `key` covers
+// the shape (first sample index, samples, batch) and every buffer, scene and kernel choice
+// baked into the nodes.
+struct RoundGraph {
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t exec = nullptr;
+  std::vector<EventPair> events;
+  unsigned long long key = 0;
+  int rounds = 0;
 };
 
 }  // namespace
@@ -815,8 +835,11 @@ struct tcmp_handle {
   DBuf<unsigned short> lodei[2];
   DBuf<float> lodev[2], geo_ev;               // link hull edge vectors (fp64 -> fp32)
   DevState* st = nullptr;
-  // plan
+  // plan: parameters on the host and their device copies (kernels read dP, so a captured
+  // round graph replays for any query of the same shape); dPx for the standalone entry points
   PlanParams P{};
+  PlanParams* dP = nullptr;
+  PlanParams* dPx = nullptr;
   bool plan_open = false;
   int max_batch = 0;
   DBuf<double> cfg, tgt;
@@ -838,7 +861,6 @@ struct tcmp_handle {
   DBuf<unsigned long long> ckey;
   DBuf<unsigned char> sort_tmp;
   DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
-  int nn_mode = 0;            // nearest scan: 0 k_nearest_wave32 (depth-first), 1 k_nearest_bfs
   int nn_waves_per_cu = 16;
   DBuf<double> second;
   DBuf<long long> chain;
@@ -851,6 +873,10 @@ struct tcmp_handle {
   // timing
   std::vector<EventPair> ev_used;
   std::vector<hipEvent_t> ev_pool;
+  RoundGraph rg;
+  unsigned long long rg_seen = 0;  // key seen once: captured when it repeats
+  bool use_graphs = true;          // TCMP_GRAPHS=0 disables; a failed capture disables
+  bool capturing = false;
   double ms[F_COUNT] = {};
   long long launches_nearest = 0;
   int edge_blocks = 0;
@@ -898,24 +924,47 @@ struct tcmp_handle {
     (void)hipEventCreate(&e);
     return e;
   }
+  // during a capture the records become external event nodes of the graph (timestamps on
+  // every replay) and the events belong to the graph
+  void record(hipEvent_t e) {
+    if (capturing) (void)hipEventRecordWithFlags(e, stream, hipEventRecordExternal);
+    else (void)hipEventRecord(e, stream);
+  }
   void mark_begin(int fam, hipEvent_t* out) {
-    *out = get_event();
-    (void)hipEventRecord(*out, stream);
+    *out = capturing ? new_event() : get_event();
+    record(*out);
     (void)fam;
   }
   void mark_end(int fam, hipEvent_t a) {
-    hipEvent_t b = get_event();
-    (void)hipEventRecord(b, stream);
-    ev_used.push_back(EventPair{a, b, fam});
+    hipEvent_t b = capturing ? new_event() : get_event();
+    record(b);
+    if (capturing) rg.events.push_back(EventPair{a, b, fam, true});
+    else ev_used.push_back(EventPair{a, b, fam, false});
+  }
+  hipEvent_t new_event() {
+    hipEvent_t e;
+    (void)hipEventCreate(&e);
+    return e;
   }
   void collect_events() {
     for (auto& p : ev_used) {
       float t = 0;
       if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) ms[p.fam] += t;
-      ev_pool.push_back(p.a);
-      ev_pool.push_back(p.b);
+      if (!p.owned) {
+        ev_pool.push_back(p.a);
+        ev_pool.push_back(p.b);
+      }
     }
     ev_used.clear();
+  }
+  void drop_graph() {
+    if (rg.exec) (void)hipGraphExecDestroy(rg.exec);
+    if (rg.graph) (void)hipGraphDestroy(rg.graph);
+    for (auto& p : rg.events) {
+      (void)hipEventDestroy(p.a);
+      (void)hipEventDestroy(p.b);
+    }
+    rg = RoundGraph{};
   }
 };
 
@@ -986,7 +1035,8 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
 // nn (index), second (a lower bound of the second-smallest score, the rewire test's input),
 // score (nullable: the winner's exact fp64 score).  The plan's rounds and tcmp_nearest both
 // come here; st is the plan's state or st_nn.
-int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const double* cfg,
+int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, DevState* st,
+                   const double* cfg,
                    long long T_bound, const double* cand, int nb, int* nn, double* second,
                    double* score) {
   hipLaunchKernelGGL(k_node_keys, dim3(std::min<unsigned>(grid_for(T_bound, 256), 4096)), dim3(256),
@@ -1053,21 +1103,12 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const doub
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
   h->mark_begin(F_NNSCAN, &e0);
-  if (h->nn_mode == 1) {
-    if (P.uniform_w)
-      hipLaunchKernelGGL(k_nearest_bfs<true>, dim3(blocks), dim3(256), 0, h->stream, P, st,
-                         h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,
-                         h->cperm.p, h->chome.p, nb, nn, second, score);
-    else
-      hipLaunchKernelGGL(k_nearest_bfs<false>, dim3(blocks), dim3(256), 0, h->stream, P, st,
-                         h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,
-                         h->cperm.p, h->chome.p, nb, nn, second, score);
-  } else if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+  if (P.uniform_w)
+    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, dP, st,
                        h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
                        h->chome.p, nb, nn, second, score);
   else
-    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, P, st,
+    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, dP, st,
                        h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
                        h->chome.p, nb, nn, second, score);
   HIPCHK(hipGetLastError());
@@ -1078,9 +1119,10 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, DevState* st, const doub
 // planned step count of each round edge (nearest node -> candidate) as an ascending sort key
 // for longest-first scheduling of k_edges
 constexpr int kEdgeOrderMin = 4096;
-__global__ void k_edge_order_keys(PlanParams P, const double* cfg, const int* nn,
+__global__ void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg, const int* nn,
                                   const double* cand, int nb, unsigned long long* keys,
                                   int* vals) {
+  const PlanParams P = *Pd;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nb) return;
   double a[7], b[7];
@@ -1092,7 +1134,7 @@ __global__ void k_edge_order_keys(PlanParams P, const double* cfg, const int* nn
 }
 
 // reset_counter = false: the plan's k_nn_home already cleared the work counter
-int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P, bool reset_counter = true) {
+int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool reset_counter = true) {
   if (J.n <= 0) return 0;
   if (reset_counter) HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
   // persistent grid bounded by residency (256-thread blocks hold one wave per SIMD each).
@@ -1104,7 +1146,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams& P, bool res
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(h->mesh_kernels() ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, P,
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, dP,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1241,9 +1283,11 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
   HIPCHK(hipMalloc(&h->st_nn, sizeof(DevState)));
+  HIPCHK(hipMalloc(&h->dP, sizeof(PlanParams)));
+  HIPCHK(hipMalloc(&h->dPx, sizeof(PlanParams)));
   HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
-  if (const char* e = getenv("TCMP_NN_MODE")) h->nn_mode = atoi(e);
+  if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
   *out = h;
   return 0;
 }
@@ -1298,12 +1342,16 @@ int tcmp_destroy(tcmp_handle* h) {
   h->chain.release();
   h->u0.release();
   for (auto& p : h->ev_used) {
+    if (p.owned) continue;
     (void)hipEventDestroy(p.a);
     (void)hipEventDestroy(p.b);
   }
+  h->drop_graph();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->st) (void)hipFree(h->st);
   if (h->st_nn) (void)hipFree(h->st_nn);
+  if (h->dP) (void)hipFree(h->dP);
+  if (h->dPx) (void)hipFree(h->dPx);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
   return 0;
@@ -1768,7 +1816,8 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
   P.torque_mode = torque_mode;
   P.mass = payload_mass;
   EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p, nullptr};
-  if ((rc = launch_edges(h, J, P))) return rc;
+  HIPCHK(hipMemcpyAsync(h->dPx, &P, sizeof(P), hipMemcpyHostToDevice, h->stream));
+  if ((rc = launch_edges(h, J, h->dPx))) return rc;
   std::vector<double> tmp((size_t)n * 8);
   HIPCHK(hipMemcpyAsync(n_safe, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(n_steps, h->i1.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
@@ -1818,7 +1867,9 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
   s.n_nodes = T;
   HIPCHK(hipMemcpyAsync(h->st_nn, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
   const size_t ev_before = h->ev_used.size();
-  rc = launch_nearest(h, P, h->st_nn, h->s0.p, T, h->s1.p, (int)n, h->i0.p, h->s2.p, nullptr);
+  HIPCHK(hipMemcpyAsync(h->dPx, &P, sizeof(P), hipMemcpyHostToDevice, h->stream));
+  rc = launch_nearest(h, P, h->dPx, h->st_nn, h->s0.p, T, h->s1.p, (int)n, h->i0.p, h->s2.p,
+                      nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -1928,6 +1979,8 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->second.ensure(B);
   rc = rc ? rc : h->rwlist.ensure(B);
   rc = rc ? rc : h->nnscore.ensure(B);
+  rc = rc ? rc : h->bcount.ensure(B / 256 + 1);
+  rc = rc ? rc : h->boff.ensure(B / 256 + 1);
   rc = rc ? rc : ensure_index(h, N, B);
   rc = rc ? rc : h->i0.ensure(2);
   if (rc) return rc;
@@ -1958,6 +2011,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   s.first_fail = -1;
   s.round_goal = INT_MAX;
   HIPCHK(hipMemcpyAsync(h->st, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->dP, &h->P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->plan_open = true;
   result->n_nodes = 1;
@@ -1966,13 +2020,67 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   return 0;
 }
 
+// identity of a captured round sequence: its shape and everything its nodes bake in
+static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samples, int batch) {
+  unsigned long long x = 1469598103934665603ull;
+  auto mix = [&](unsigned long long v) {
+    for (int i = 0; i < 8; ++i) {
+      x ^= (v >> (8 * i)) & 0xffull;
+      x *= 1099511628211ull;
+    }
+  };
+  auto mixp = [&](const void* p) { mix((unsigned long long)(uintptr_t)p); };
+  mix((unsigned long long)h->samples_issued);
+  mix((unsigned long long)n_samples);
+  mix((unsigned long long)batch);
+  mix((unsigned long long)h->P.uniform_w);
+  mix((unsigned long long)h->mesh_kernels());
+  mix((unsigned long long)lds_bytes(h));
+  mix((unsigned long long)h->nn_waves_per_cu);
+  mix((unsigned long long)h->sort_tmp.n);
+  for (const void* p : {(const void*)h->cfg.p, (const void*)h->tgt.p, (const void*)h->parent.p,
+                        (const void*)h->meta.p, (const void*)h->cand.p, (const void*)h->last.p,
+                        (const void*)h->cgoal.p, (const void*)h->nn.p, (const void*)h->nsafe.p,
+                        (const void*)h->nsteps.p, (const void*)h->nbr.p, (const void*)h->ncount.p,
+                        (const void*)h->second.p, (const void*)h->rwlist.p, (const void*)h->nnscore.p,
+                        (const void*)h->nkeys_in.p, (const void*)h->skeys.p, (const void*)h->nvals_in.p,
+                        (const void*)h->svals.p, (const void*)h->stree.p, (const void*)h->stree32.p,
+                        (const void*)h->cboxf.p, (const void*)h->sboxf.p, (const void*)h->bboxf.p,
+                        (const void*)h->cflag.p, (const void*)h->cid.p, (const void*)h->cstart.p,
+                        (const void*)h->sflag.p, (const void*)h->sid.p, (const void*)h->sstart.p,
+                        (const void*)h->ckey.p, (const void*)h->chome.p, (const void*)h->ckeys_in.p,
+                        (const void*)h->ckeys.p, (const void*)h->cvals_in.p, (const void*)h->cperm.p,
+                        (const void*)h->sort_tmp.p, (const void*)h->bcount.p, (const void*)h->boff.p,
+                        (const void*)h->st, (const void*)h->dP})
+    mixp(p);
+  const Scene sc = h->scene();
+  const Geo g = h->geo();
+  const unsigned char* b = reinterpret_cast<const unsigned char*>(&sc);
+  for (size_t i = 0; i < sizeof(sc); ++i) mix(b[i]);
+  b = reinterpret_cast<const unsigned char*>(&g);
+  for (size_t i = 0; i < sizeof(g); ++i) mix(b[i]);
+  return x;
+}
+
 static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t* is_goal,
                            int32_t nb) {
   const PlanParams& P = h->P;
   if (samples) {
     std::vector<double> tmp((size_t)nb * 8, 0.0);
+    double cmax = 0.0;
     for (int j = 0; j < nb; ++j)
-      for (int k = 0; k < 7; ++k) tmp[8 * j + k] = samples[7 * j + k];
+      for (int k = 0; k < 7; ++k) {
+        const double x = samples[7 * j + k];
+        if (!std::isfinite(x)) return fail(-1, "non-finite sample coordinate");
+        cmax = std::max(cmax, fabs(x));
+        tmp[8 * j + k] = x;
+      }
+    if (cmax > h->P.nn_cmax) {
+      // a caller's sampler reached outside the joint-limit box: widen the nearest scan's
+      // fp32 error terms (tcmp_nn32.h) so it stays exact
+      h->P.nn_cmax = cmax * (1.0 + 1e-6);
+      HIPCHK(hipMemcpyAsync(h->dP, &h->P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
+    }
     HIPCHK(hipMemcpyAsync(h->cand.p, tmp.data(), tmp.size() * sizeof(double),
                           hipMemcpyHostToDevice, h->stream));
     std::vector<unsigned char> g((size_t)nb, 0);
@@ -1981,7 +2089,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
     HIPCHK(hipMemcpyAsync(h->cgoal.p, g.data(), nb, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
   } else {
-    hipLaunchKernelGGL(k_sample, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+    hipLaunchKernelGGL(k_sample, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
                        (long long)h->samples_issued, nb, h->cand.p, h->cgoal.p);
     HIPCHK(hipGetLastError());
   }
@@ -1990,14 +2098,14 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   hipEvent_t e0;
   h->mark_begin(F_NEAREST, &e0);
   if (!samples) {
-    hipLaunchKernelGGL(k_goal_fix, dim3(1), dim3(64), 0, h->stream, P, h->st, h->cand.p,
+    hipLaunchKernelGGL(k_goal_fix, dim3(1), dim3(64), 0, h->stream, h->dP, h->st, h->cand.p,
                        h->cgoal.p, nb);
     HIPCHK(hipGetLastError());
   }
   // the snapshot holds at most 1 + (samples issued before this round) nodes
   {
     const long long T_bound = 1 + h->samples_issued - nb;
-    if (int rc = launch_nearest(h, P, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
+    if (int rc = launch_nearest(h, P, h->dP, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
                                 h->second.p, h->nnscore.p))
       return rc;
   }
@@ -2009,7 +2117,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   if (nb >= kEdgeOrderMin) {
     // longest planned edges first (the persistent lanes then finish together): 8-bit keys
     // 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
-    hipLaunchKernelGGL(k_edge_order_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P,
+    hipLaunchKernelGGL(k_edge_order_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP,
                        h->cfg.p, h->nn.p, h->cand.p, nb, h->ckeys_in.p, h->cvals_in.p);
     HIPCHK(hipGetLastError());
     size_t tb = h->sort_tmp.n;
@@ -2018,7 +2126,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
                                                h->stream));
     J.order = h->cperm.p;
   }
-  if (int rc = launch_edges(h, J, P, false)) return rc;
+  if (int rc = launch_edges(h, J, h->dP, false)) return rc;
   h->mark_end(F_EDGES, e0);
   h->mark_begin(F_INSERT, &e0);
   {
@@ -2029,18 +2137,18 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
                        h->bcount.p);
     hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
                        h->boff.p);
-    hipLaunchKernelGGL(k_ins_write, dim3(nblk), dim3(256), 0, h->stream, P, h->st, tr, h->nn.p,
+    hipLaunchKernelGGL(k_ins_write, dim3(nblk), dim3(256), 0, h->stream, h->dP, h->st, tr, h->nn.p,
                        h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->boff.p,
                        h->second.p, h->rwlist.p);
-    hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, P, h->st, nb);
+    hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, h->dP, h->st, nb);
     HIPCHK(hipGetLastError());
   }
   h->mark_end(F_INSERT, e0);
   h->mark_begin(F_REWIRE, &e0);
-  hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, P, h->st,
+  hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());
-  hipLaunchKernelGGL(h->mesh_kernels() ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), lds_bytes(h), h->stream, P, h->st,
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_rewire_apply<true> : k_rewire_apply<false>, dim3(grid_for(nb, 256)), dim3(256), lds_bytes(h), h->stream, h->dP, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p, h->scene(), h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, e0);
@@ -2068,12 +2176,59 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
   if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
   if (batch < 1 || batch > h->max_batch) return fail(-1, "batch size out of range");
   if (h->samples_issued + n_samples + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
-  long long left = n_samples;
-  while (left > 0) {
-    const int nb = (int)std::min<long long>(left, batch);
-    if (int rc = plan_round_impl(h, nullptr, nullptr, nb)) return rc;
-    left -= nb;
+  auto run_rounds = [&]() -> int {
+    long long left = n_samples;
+    while (left > 0) {
+      const int nb = (int)std::min<long long>(left, batch);
+      if (int rc = plan_round_impl(h, nullptr, nullptr, nb)) return rc;
+      left -= nb;
+    }
+    return 0;
+  };
+  if (!h->use_graphs || n_samples <= 0) return run_rounds();
+  const unsigned long long key = round_graph_key(h, n_samples, batch);
+  if (!(h->rg.exec && h->rg.key == key)) {
+    if (h->rg_seen != key) {  // first sight of this shape: launch directly, capture next time
+      h->rg_seen = key;
+      return run_rounds();
+    }
+    h->drop_graph();
+    const long long issued = h->samples_issued, launches = h->launches_nearest;
+    const int last_nb = h->last_nb;
+    int rc = 0;
+    if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
+      rc = -2;
+    } else {
+      h->capturing = true;
+      rc = run_rounds();
+      h->capturing = false;
+      hipGraph_t g = nullptr;
+      const hipError_t e = hipStreamEndCapture(h->stream, &g);
+      if (rc == 0 && e == hipSuccess && g &&
+          hipGraphInstantiate(&h->rg.exec, g, nullptr, nullptr, 0) == hipSuccess) {
+        h->rg.graph = g;
+        h->rg.key = key;
+        h->rg.rounds = (int)(h->launches_nearest - launches);
+      } else {
+        if (g) (void)hipGraphDestroy(g);
+        h->drop_graph();
+        rc = rc ? rc : -2;
+      }
+    }
+    (void)hipGetLastError();
+    h->samples_issued = issued;  // nothing ran yet
+    h->launches_nearest = launches;
+    h->last_nb = last_nb;
+    if (rc) {  // capture unsupported here: launch directly from now on
+      h->use_graphs = false;
+      return run_rounds();
+    }
   }
+  HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
+  h->samples_issued += n_samples;
+  h->launches_nearest += h->rg.rounds;
+  h->last_nb = (int)(n_samples % batch ? n_samples % batch : batch);
+  for (const auto& p : h->rg.events) h->ev_used.push_back(p);
   return 0;
 }
 
@@ -2095,7 +2250,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
     if (rc) return rc;
     hipEvent_t e0;
     h->mark_begin(F_FINISH, &e0);
-    hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->P, h->st,
+    hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->dP, h->st,
                        Tree{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p}, h->chain.p, h->wp.p,
                        (long long)(h->wp.n / 7));
     HIPCHK(hipGetLastError());
@@ -2111,7 +2266,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
     if (rc) return rc;
     hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
     hipLaunchKernelGGL(k_traj, dim3(std::min<unsigned>(grid_for(K, 256), 2048)), dim3(256), 0,
-                       h->stream, h->P, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
+                       h->stream, h->dP, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
                        h->ttau.p);
     hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
     HIPCHK(hipGetLastError());

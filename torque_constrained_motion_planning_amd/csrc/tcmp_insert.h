@@ -42,12 +42,13 @@ __global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcou
   }
 }
 
-__global__ __launch_bounds__(256) void k_ins_write(PlanParams P, DevState* st, Tree tr,
+__global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
                                                    const int* nn, const double* cand,
                                                    const unsigned char* cgoal, const int* nsafe,
                                                    const int* nsteps, const double* last, int nb,
                                                    const int* boff, const double* second,
                                                    int* rwlist) {
+  const PlanParams P = *Pd;
   __shared__ int wc[4];
   const long long T = st->n_nodes;
   const long long total = st->ins_total;
@@ -89,7 +90,8 @@ __global__ __launch_bounds__(256) void k_ins_write(PlanParams P, DevState* st, T
   if (second[j] < t * t * (1.0 + 1e-9) + 1e-300) rwlist[atomicAdd(&st->rw_count, 1)] = (int)idx;
 }
 
-__global__ void k_ins_final(PlanParams P, DevState* st, int nb) {
+__global__ void k_ins_final(const PlanParams* __restrict__ Pd, DevState* st, int nb) {
+  const PlanParams P = *Pd;
   const long long T = st->n_nodes, total = st->ins_total;
   st->snap = T;
   if (T + total > P.max_nodes) {

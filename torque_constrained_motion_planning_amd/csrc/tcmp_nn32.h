@@ -62,13 +62,14 @@ __device__ __forceinline__ float box_lb32(const float* b, const float s[7], cons
 #define TCMP_NN_MINB 1  // min 256-thread blocks per CU the register allocation must allow
 #endif
 template <bool UW>
-__global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(PlanParams P, DevState* st,
+__global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
                                                         const float* sbox, const float* bbox,
                                                         const double* cand,
                                                         const int* cperm, const int* home, int nb,
                                                         int* nn, double* second, double* score) {
+  const PlanParams P = *Pd;
   const int lane = lane_id();
   const long long T = st->n_nodes;
   const int nch = st->nn_cells, nsup = st->nn_supers;
