@@ -1103,14 +1103,13 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
   h->mark_begin(F_NNSCAN, &e0);
-  if (P.uniform_w)
-    hipLaunchKernelGGL(k_nearest_wave32<true>, dim3(blocks), dim3(256), 0, h->stream, dP, st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
-                       h->chome.p, nb, nn, second, score);
-  else
-    hipLaunchKernelGGL(k_nearest_wave32<false>, dim3(blocks), dim3(256), 0, h->stream, dP, st,
-                       h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand, h->cperm.p,
-                       h->chome.p, nb, nn, second, score);
+#define TCMP_NNW(UWV, SWV)                                                                   \
+  hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(256), 0, h->stream, dP, st, \
+                     h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,          \
+                     h->cperm.p, h->chome.p, nb, nn, second, score)
+  // four cells per scan round (eight measured slower: 137 VGPRs cost a wave per SIMD)
+  if (P.uniform_w) TCMP_NNW(true, 4); else TCMP_NNW(false, 4);
+#undef TCMP_NNW
   HIPCHK(hipGetLastError());
   h->mark_end(F_NNSCAN, e0);
   return 0;

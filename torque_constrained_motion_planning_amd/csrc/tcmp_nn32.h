@@ -61,7 +61,10 @@ __device__ __forceinline__ float box_lb32(const float* b, const float s[7], cons
 #ifndef TCMP_NN_MINB
 #define TCMP_NN_MINB 1  // min 256-thread blocks per CU the register allocation must allow
 #endif
-template <bool UW>
+// SW: cells per scan round (4 or 8).  Passing cells queue up across super-cells (the queue
+// holds at most SW) and a round loads all their rows at once: fewer dependent round trips
+// per candidate than one round per super-cell.
+template <bool UW, int SW>
 __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
@@ -214,13 +217,13 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
       Rf = tr * tr * kRfac;
       return t * t * 1.000003f;
     };
-    // up to four cells (count 0 = none), all row loads in flight before any use
-    auto scan4 = [&](const int cs[4], const int cn[4]) {
-      float4 A[4], Bq[4];
-      bool val[4];
+    // up to SW cells (count 0 = none), all row loads in flight before any use
+    auto scanw = [&](const int cs[SW], const int cn[SW]) {
+      float4 A[SW], Bq[SW];
+      bool val[SW];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        // wave-uniform row base + lane offset: scalar-base loads, no per-lane 64-bit math
+      for (int u = 0; u < SW; ++u) {
+        // wave-uniform row base + lane offset
         const int c0 = __builtin_amdgcn_readfirstlane(cs[u]);
         const int cnt = __builtin_amdgcn_readfirstlane(cn[u]);
         const float4* rp = reinterpret_cast<const float4*>(stree32) + 2 * (unsigned)c0;
@@ -232,11 +235,29 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
         pairs += (unsigned long long)cnt;
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
+      for (int u = 0; u < SW; ++u)
         if (val[u]) upd(A[u], Bq[u], (long long)cs[u] + lane);
       return refresh();
     };
+    // queue of passing cells (wave-uniform), scanned SW at a time
+    int pcs[SW], pcn[SW], np = 0;
+#pragma unroll
+    for (int u = 0; u < SW; ++u) { pcs[u] = 0; pcn[u] = 0; }
     float thr;
+    auto flush = [&]() {
+      if (np) {
+        thr = scanw(pcs, pcn);
+        np = 0;
+#pragma unroll
+        for (int u = 0; u < SW; ++u) pcn[u] = 0;
+      }
+    };
+    auto push = [&](int cs, int cn) {
+#pragma unroll
+      for (int u = 0; u < SW; ++u)
+        if (u == np) { pcs[u] = cs; pcn[u] = cn; }
+      if (++np == SW) flush();
+    };
     {
       // home cell: R = inf, every node exact
       if (lane < hcn) refine((long long)hcs + lane);
@@ -278,27 +299,16 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
           uint64_t cmask = __ballot(lbc <= thr);
           NN_TICK(2);
           while (cmask) {
-            int cs4[4], cn4[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-              cs4[u] = 0;
-              cn4[u] = 0;
-              while (cmask) {
-                const int k = __builtin_ctzll(cmask);
-                cmask &= cmask - 1;
-                if (readlane_f(lbc, k) <= thr) {
-                  cs4[u] = __builtin_amdgcn_readlane(cst, k);
-                  cn4[u] = __builtin_amdgcn_readlane(ccn, k);
-                  break;
-                }
-              }
-            }
-            if (cn4[0] > 0) thr = scan4(cs4, cn4);
-            NN_TICK(3);
+            const int k = __builtin_ctzll(cmask);
+            cmask &= cmask - 1;
+            if (readlane_f(lbc, k) <= thr)
+              push(__builtin_amdgcn_readlane(cst, k), __builtin_amdgcn_readlane(ccn, k));
           }
+          NN_TICK(3);
         }
       }
     }
+    flush();
     const double m = wave_min(b1);
     const int wi = wave_min_int(b1 == m ? bi : INT_MAX);
     const bool winner = (b1 == m) && (bi == wi);
