@@ -19,13 +19,16 @@ def main():
     obs, _, goal = bench.make_query(1234, engine=eng)
     for q in range(n):
         r, _ = bench.run_query(eng, obs, goal, 1_000_000, 262144, 1234 + q)
-        c = eng.debug_counters(13)[8:13]
+        cc = eng.debug_counters(44)
+        c, v = cc[36:41], cc[41:44]
         tot = max(1, sum(c))
         print(json.dumps({"query": q, "ms_nn_scan": r.ms_nn_scan, "nn_pairs": r.nn_pairs,
                           "nn_box_tests": r.nn_box_tests,
                           "setup_home": c[0] / tot, "super_bounds": c[1] / tot,
                           "chunk_bounds": c[2] / tot, "chunk_scans": c[3] / tot,
-                          "final": c[4] / tot}), flush=True)
+                          "final": c[4] / tot,
+                          "super_box_wave_tests": v[0], "cell_box_wave_tests": v[1],
+                          "cells_scanned": v[2]}), flush=True)
 
 
 if __name__ == "__main__":

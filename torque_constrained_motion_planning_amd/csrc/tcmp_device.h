@@ -127,7 +127,12 @@ __device__ __forceinline__ int obs_mesh(const double* ob) {
   return ob[15] < 0.0 ? (int)(-ob[15]) - 1 : -1;
 }
 constexpr int kQcap = 128;           // queued (lane, link, obstacle) pairs per wave
-constexpr unsigned kQwaveBytes = (kQcap + 2) * 4;
+// per wave: the pair queue, the wave's collision mask (u64) and a 12-double pose slot that hands
+// a pair's link pose to the out-of-line fp64 exact tests (so no argument goes through scratch)
+constexpr unsigned kQwaveBytes = (kQcap + 2) * 4 + 12 * 8;
+__device__ __forceinline__ double* wave_pose_slot(unsigned* wq) {
+  return reinterpret_cast<double*>(wq + kQcap + 2);
+}
 
 // Obstacle records and the fp32 hull geometry are staged in LDS by every kernel that runs
 // collision checks (dynamic shared memory, stage_lds_bytes(n) per block): the per-(link,
@@ -459,11 +464,18 @@ struct Pose {
   double p[3];
 };
 
-__device__ __noinline__ double exact_pd_wave(int link, const Pose pose,
-                                             const double* __restrict__ ob, const Geo g) {
+// pose: R[9], p[3] in the wave's LDS pose slot (wave_pose_slot); the geometry pointers are
+// passed one by one, so every argument travels in registers
+__device__ __noinline__ double exact_pd_wave(int link, const double* pose,
+                                             const double* __restrict__ ob,
+                                             const double* __restrict__ gverts,
+                                             const double* __restrict__ gplanes,
+                                             const double* __restrict__ gedges) {
   const int lane = lane_id();
-  const double* R = pose.R;
-  const double* p = pose.p;
+  const double* R = pose;
+  const double* p = pose + 9;
+  const struct { const double* verts; const double* planes; const double* edges; } g = {
+      gverts, gplanes, gedges};
   // box in the link frame
   const double d[3] = {ob[0] - p[0], ob[1] - p[1], ob[2] - p[2]};
   double cl[3], A[9];
@@ -554,6 +566,20 @@ __device__ __forceinline__ float wave_minf(float x) {
   x = fminf(x, dpp_f<0x124>(x));
   x = fminf(x, dpp_f<0x128>(x));
   return fminf(fminf(readlane_f(x, 0), readlane_f(x, 16)), fminf(readlane_f(x, 32), readlane_f(x, 48)));
+}
+// the same minimum with the cross-row steps in DPP as well: row_bcast:15 folds rows 0 -> 1 and
+// 2 -> 3, row_bcast:31 folds row 1 -> rows 2 and 3, so lane 63 holds the wave minimum and one
+// readlane returns it (the rows' disabled lanes keep their own value through `old`)
+__device__ __forceinline__ float wave_minf_bc(float x) {
+  x = fminf(x, dpp_f<0xB1>(x));
+  x = fminf(x, dpp_f<0x4E>(x));
+  x = fminf(x, dpp_f<0x124>(x));
+  x = fminf(x, dpp_f<0x128>(x));
+  x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
+                                                          0x142, 0xA, 0xF, false)));
+  x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
+                                                          0x143, 0xC, 0xF, false)));
+  return readlane_f(x, 63);
 }
 __device__ __forceinline__ float wave_maxf(float x) {
   x = fmaxf(x, dpp_f<0xB1>(x));
@@ -711,10 +737,22 @@ template <bool MESH>
 __device__ __forceinline__ double exact_pair(int link, const Pose PL, const double* ob,
                                              const Scene sc, const Geo g) {
   const int mi = MESH ? obs_mesh(ob) : -1;
+  // the fp64 restatements are out of line; the pose reaches them through the wave's LDS slot
+  auto pose_to_lds = [&]() {
+    double* slot = wave_pose_slot(sc.wq);
+    if (lane_id() == 0) {
+#pragma unroll
+      for (int k = 0; k < 9; ++k) slot[k] = PL.R[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) slot[9 + k] = PL.p[k];
+    }
+    __builtin_amdgcn_wave_barrier();
+    return (const double*)slot;
+  };
   if (!MESH || mi < 0) {
     const float pd32 = exact_pd_wave32(link, PL, ob, g);
-    return (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) ? (double)pd32
-                                                                      : exact_pd_wave(link, PL, ob, g);
+    if (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) return (double)pd32;
+    return exact_pd_wave(link, pose_to_lds(), ob, g.verts, g.planes, g.edges);
   }
 #ifdef TCMP_PROF_EXACT
 #define TCMP_MESH_STAT(i) if (lane_id() == 0) atomicAdd(&g_exact_stats[i], 1ull)
@@ -769,7 +807,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
   TCMP_MESH_CLK(3);
   if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;
   TCMP_MESH_STAT(7);
-  const double r64 = exact_mesh_wave(link, PL, mi, sc, g);
+  const double r64 = exact_mesh_wave(link, pose_to_lds(), mi, sc.mrange, sc.mp64, sc.mv64, sc.me64,
+                                     g.verts, g.planes, g.edges);
   TCMP_MESH_CLK(4);
   return r64;
 #undef TCMP_MESH_STAT

@@ -84,6 +84,7 @@ struct DevState {
   int nn_cells;          // cells of the current nearest-neighbour index (k_nn_starts)
   int nn_supers;         // super-cells of the index
   unsigned long long prof[16];  // TCMP_PROF builds: k_edges clock breakdown + exact-test stats
+  unsigned long long prof_nn[8]; // TCMP_PROF builds: nearest-scan clocks [0..4] and visit counts [5..7]
 };
 
 struct PlanParams {
@@ -862,6 +863,7 @@ struct tcmp_handle {
   DBuf<unsigned char> sort_tmp;
   DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
   int nn_waves_per_cu = 16;
+  int nn_cand_bits = 16;           // top key bits the candidates are sorted by
   DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
@@ -1091,7 +1093,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                              h->cvals_in.p, h->cperm.p, (size_t)nb,
-                                             kKeyBits + 1 - 16, kKeyBits + 1,
+                                             kKeyBits + 1 - h->nn_cand_bits, kKeyBits + 1,
                                              h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
                      h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
@@ -1178,16 +1180,17 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (int rc = set_dev(h)) return rc;
-  if (!out || n < 0 || n > 36) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 44) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   // prof[] has 16 entries; 12..35 are the exact-test stats of TCMP_PROF_EXACT builds
-  for (int i = 0; i < n; ++i) out[i] = i < 16 ? s.prof[i] : 0;
+  // 36..43 are the nearest scan's clocks and visit counts (prof_nn)
+  for (int i = 0; i < n; ++i) out[i] = i < 16 ? s.prof[i] : i >= 36 ? s.prof_nn[i - 36] : 0;
 #ifdef TCMP_PROF_EXACT
   unsigned long long ex[24];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
-  for (int i = 0; i < 24 && 12 + i < n; ++i) out[12 + i] = ex[i];
+  for (int i = 0; i < 24 && 12 + i < n && 12 + i < 36; ++i) out[12 + i] = ex[i];
 #endif
   return 0;
 }
@@ -1287,6 +1290,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
+  if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(kKeyBits + 1, std::max(8, atoi(e)));
   *out = h;
   return 0;
 }
@@ -2036,6 +2040,7 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
   mix((unsigned long long)h->mesh_kernels());
   mix((unsigned long long)lds_bytes(h));
   mix((unsigned long long)h->nn_waves_per_cu);
+  mix((unsigned long long)h->nn_cand_bits);
   mix((unsigned long long)h->sort_tmp.n);
   for (const void* p : {(const void*)h->cfg.p, (const void*)h->tgt.p, (const void*)h->parent.p,
                         (const void*)h->meta.p, (const void*)h->cand.p, (const void*)h->last.p,

@@ -207,16 +207,27 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
 
 // fp64 restatement of hull_hull_wave32 on the full hulls (same axes, strict Gauss-map test, no degeneracy
 // shortcuts): the decision-maker near kPen.  Every lane of the wave calls it.
-__device__ __noinline__ double exact_mesh_wave(int link, const Pose pose, int m, const Scene sc,
-                                               const Geo g) {
+// pose: R[9], p[3] in the wave's LDS pose slot; pointers one by one (no argument in scratch)
+__device__ __noinline__ double exact_mesh_wave(int link, const double* pose, int m,
+                                               const int* __restrict__ mrange,
+                                               const double4* __restrict__ mp64,
+                                               const double4* __restrict__ mv64,
+                                               const double* __restrict__ me64,
+                                               const double* __restrict__ gverts,
+                                               const double* __restrict__ gplanes,
+                                               const double* __restrict__ gedges) {
   const int lane = lane_id();
-  const int* rg = sc.mrange + kMrange * m;
+  const struct { const double* verts; const double* planes; const double* edges; } g = {
+      gverts, gplanes, gedges};
+  const struct { const double4* mp64; const double4* mv64; const double* me64; } sc = {mp64, mv64,
+                                                                                         me64};
+  const int* rg = mrange + kMrange * m;
   const int v0 = rg[0], v1 = rg[1], f0 = rg[2], f1 = rg[3], e0 = rg[4], e1 = rg[5];
   const int lv0 = tcmp_geo_vert_off[link], lv1 = tcmp_geo_vert_off[link + 1];
   const int lf0 = tcmp_geo_plane_off[link], lf1 = tcmp_geo_plane_off[link + 1];
   const int le0 = tcmp_geo_edge_off[link], le1 = tcmp_geo_edge_off[link + 1];
-  const double* R = pose.R;
-  const double* p = pose.p;
+  const double* R = pose;
+  const double* p = pose + 9;
   double loc = INFINITY;
   for (int f = f0 + lane; f < f1; f += 64) {
     const double4 w = sc.mp64[f];

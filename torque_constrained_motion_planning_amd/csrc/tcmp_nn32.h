@@ -34,12 +34,14 @@ __device__ __forceinline__ unsigned xcc_id() {
 }
 
 // Lower bound of the weighted squared distance from s to a float box, in fp32, never above
-// the exact value: each gap is shrunk by `gap` = 1.25e-7 cmax (> the fp32 rounding of s and
-// of the subtraction for |q| <= cmax; 1e-6 on the planner's path) and the sum by 1e-6
-// relative.
+// the exact value.  sh = s32 + G and sl = s32 - G (rounded to nearest) with G = 8 u cmax:
+// |s32 - s| <= u cmax and the roundings of sh, sl and of the two subtractions add at most
+// 3 u cmax more, so each computed gap max(lo - sh, sl - hi, 0) stays below the exact gap
+// max(lo - s, s - hi, 0); the weighted sum of squares is scaled down by 1e-6 relative to cover
+// its own rounding.
 template <bool UW>
-__device__ __forceinline__ float box_lb32(const float* b, const float s[7], const float w[7],
-                                          float gap, int* start = nullptr,
+__device__ __forceinline__ float box_lb32(const float* b, const float sh[7], const float sl[7],
+                                          const float w[7], int* start = nullptr,
                                           int* count = nullptr) {
   const float4 l0 = *reinterpret_cast<const float4*>(b);
   const float4 l1 = *reinterpret_cast<const float4*>(b + 4);
@@ -52,7 +54,7 @@ __device__ __forceinline__ float box_lb32(const float* b, const float s[7], cons
   float lb = 0.f;
 #pragma unroll
   for (int k = 0; k < 7; ++k) {
-    const float g = fmaxf(0.f, fmaxf(lo[k] - s[k], s[k] - hi[k]) - gap);
+    const float g = fmaxf(fmaxf(lo[k] - sh[k], sl[k] - hi[k]), 0.f);
     lb = fmaf(UW ? g : w[k] * g, g, lb);
   }
   return lb * 0.999999f;
@@ -85,7 +87,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     wsum += w[k];
   }
   const double E = 4.0 * kNnU32 * P.nn_cmax * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
-  const float gap = (float)(1.25e-7 * P.nn_cmax);
+  const float G = (float)(8.0 * kNnU32 * P.nn_cmax);  // box_lb32's coordinate shift
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
   const float E32 = __double2float_ru(E * (1.0 + 1e-9)), ru32 = __double2float_ru(ru);
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
@@ -94,6 +96,9 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
   // clocks: [0] setup + home chunk, [1] super-chunk bounds, [2] chunk bounds, [3] chunk scans,
   // [4] final reduction
   unsigned long long pc[5] = {0, 0, 0, 0, 0};
+  // visits: [0] super-cell box wave tests (passing blocks), [1] cell box wave tests (passing
+  // super-cells), [2] cells pushed to the scan queue
+  unsigned long long pv[3] = {0, 0, 0};
   unsigned long long t0 = clock64();
 #define NN_TICK(k) { const unsigned long long t1 = clock64(); pc[k] += t1 - t0; t0 = t1; }
 #else
@@ -145,9 +150,13 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     double s[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) s[k] = readlane_d(sl[k], ib);
-    float s32[7];
+    float s32[7], sh[7], sl32[7];
 #pragma unroll
-    for (int k = 0; k < 7; ++k) s32[k] = (float)s[k];
+    for (int k = 0; k < 7; ++k) {
+      s32[k] = (float)s[k];
+      sh[k] = s32[k] + G;
+      sl32[k] = s32[k] - G;
+    }
     const int hc = __builtin_amdgcn_readlane(hml, ib);
     const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
     const int hs = __builtin_amdgcn_readlane(hsu, ib);
@@ -155,6 +164,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     int bi = INT_MAX;
     float r2 = INFINITY;   // smallest fp32 value among this lane's unrefined nodes
     float Rf = INFINITY;   // refine threshold R(m) (wave-uniform)
+    bool imp = false;      // this lane's exact best improved since the last refresh
     auto refine = [&](long long n) {
       const double* nd = stree + 8 * n;
       const double4 a = *reinterpret_cast<const double4*>(nd);
@@ -176,6 +186,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
         b2 = b1;
         b1 = dd;
         bi = idx;
+        imp = true;
       } else {
         b2 = fmin(b2, dd);
       }
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
                 s6 = {s32[6], 0.f};
     const f32x2 w01 = {w32[0], w32[1]}, w23 = {w32[2], w32[3]}, w45 = {w32[4], w32[5]},
                 w6 = {w32[6], 0.f};
-    auto upd = [&](const float4 a, const float4 b, long long n) {
+    auto dist32 = [&](const float4 a, const float4 b) {
       const f32x2 d01 = s01 - f32x2{a.x, a.y}, d23 = s23 - f32x2{a.z, a.w},
                   d45 = s45 - f32x2{b.x, b.y}, d6 = s6 - f32x2{b.z, 0.f};
       f32x2 acc;
@@ -201,16 +212,14 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
         acc = __builtin_elementwise_fma(w45 * d45, d45, acc);
         acc = __builtin_elementwise_fma(w6 * d6, d6, acc);
       }
-      const float r = acc.x + acc.y;
-      if (r <= Rf) refine(n);
-      else r2 = fminf(r2, r);
+      return acc.x + acc.y;
     };
     // refresh the pruning threshold and the refine threshold from the exact best m, in fp32
     // rounded upward (m32 >= m, so both thresholds only grow: pruning and refinement stay
     // conservative)
     auto refresh = [&]() {
       // (each round-to-nearest step is covered by a 1e-6 relative margin, >> 2^-24)
-      const float m32 = wave_minf(__double2float_ru(b1));
+      const float m32 = wave_minf_bc(__double2float_ru(b1));
       const float sm = sqrtf(m32) * 1.000001f;
       const float t = (sm + ru32) * 1.000001f;
       const float tr = (sm + E32) * 1.000001f;
@@ -218,7 +227,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
       return t * t * 1.000003f;
     };
     // up to SW cells (count 0 = none), all row loads in flight before any use
-    auto scanw = [&](const int cs[SW], const int cn[SW]) {
+    auto scanw = [&](const int cs[SW], const int cn[SW]) -> void {
       float4 A[SW], Bq[SW];
       bool val[SW];
 #pragma unroll
@@ -234,10 +243,23 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
         }
         pairs += (unsigned long long)cnt;
       }
+      // the SW distances first, then one branch: refinement (r <= Rf) is the rare case
+      float r[SW];
+      float rm = INFINITY;
 #pragma unroll
-      for (int u = 0; u < SW; ++u)
-        if (val[u]) upd(A[u], Bq[u], (long long)cs[u] + lane);
-      return refresh();
+      for (int u = 0; u < SW; ++u) {
+        r[u] = val[u] ? dist32(A[u], Bq[u]) : INFINITY;
+        rm = fminf(rm, r[u]);
+      }
+      if (rm <= Rf) {
+#pragma unroll
+        for (int u = 0; u < SW; ++u) {
+          if (r[u] <= Rf) refine((long long)cs[u] + lane);
+          else r2 = fminf(r2, r[u]);
+        }
+      } else {
+        r2 = fminf(r2, rm);
+      }
     };
     // queue of passing cells (wave-uniform), scanned SW at a time
     int pcs[SW], pcn[SW], np = 0;
@@ -246,7 +268,12 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     float thr;
     auto flush = [&]() {
       if (np) {
-        thr = scanw(pcs, pcn);
+        scanw(pcs, pcn);
+        // the thresholds only move when some lane's exact best improved
+        if (__ballot(imp)) {
+          thr = refresh();
+          imp = false;
+        }
         np = 0;
 #pragma unroll
         for (int u = 0; u < SW; ++u) pcn[u] = 0;
@@ -263,6 +290,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
       if (lane < hcn) refine((long long)hcs + lane);
       pairs += (unsigned long long)hcn;
       thr = refresh();
+      imp = false;
     }
     NN_TICK(0);
     // blocks of 64 super-cells, zig-zagging out from the home block (one box test each);
@@ -270,7 +298,7 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
     for (int gb = 0; gb < nblk; gb += 64) {
       const int bidx = zigzag(hb, gb + lane, nblk);
-      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, s32, w32, gap) : INFINITY;
+      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, sh, sl32, w32) : INFINITY;
       tests += (unsigned long long)min(64, nblk - gb);
       uint64_t bmask = __ballot(lbb <= thr);
       while (bmask) {
@@ -282,8 +310,11 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
         const int sidx = 64 * blk + ((lane + rot) & 63);
         int sc0 = 0, scn = 0;
         const float lbs =
-            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, s32, w32, gap, &sc0, &scn) : INFINITY;
+            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
         tests += (unsigned long long)min(64, nsup - 64 * blk);
+#ifdef TCMP_PROF
+        ++pv[0];
+#endif
         uint64_t smask = __ballot(lbs <= thr);
         NN_TICK(1);
         while (smask) {
@@ -294,15 +325,22 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
           const int c = S0 + lane;
           const bool cv = lane < Sn && c != hc;
           int cst = 0, ccn = 0;
-          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, s32, w32, gap, &cst, &ccn) : INFINITY;
+          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, sh, sl32, w32, &cst, &ccn) : INFINITY;
           tests += (unsigned long long)Sn;
+#ifdef TCMP_PROF
+          ++pv[1];
+#endif
           uint64_t cmask = __ballot(lbc <= thr);
           NN_TICK(2);
           while (cmask) {
             const int k = __builtin_ctzll(cmask);
             cmask &= cmask - 1;
-            if (readlane_f(lbc, k) <= thr)
+            if (readlane_f(lbc, k) <= thr) {
+#ifdef TCMP_PROF
+              ++pv[2];
+#endif
               push(__builtin_amdgcn_readlane(cst, k), __builtin_amdgcn_readlane(ccn, k));
+            }
           }
           NN_TICK(3);
         }
@@ -340,8 +378,10 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
     atomicAdd(&st->nn_pairs, pairs);
     atomicAdd(&st->nn_box_tests, tests);
 #ifdef TCMP_PROF
-    for (int k = 0; k < 5; ++k) atomicAdd(&st->prof[8 + k], pc[k]);
+    for (int k = 0; k < 5; ++k) atomicAdd(&st->prof_nn[k], pc[k]);
+    for (int k = 0; k < 3; ++k) atomicAdd(&st->prof_nn[5 + k], pv[k]);
 #endif
   }
 #undef NN_TICK
 }
+
