@@ -132,13 +132,19 @@ def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None, n_me
 
 
 def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass=5.0,
-              exec_time=5.0, meshes=None):
+              exec_time=5.0, meshes=None, shared=None):
+    """One planning query.  shared: a communicator -- the ranks then grow ONE tree together
+    (tcmp_plan_run_shared: each rank takes its share of every round's lanes)."""
     eng.set_scene(obs, meshes)
+    world = shared.world if shared is not None else 1
     st = eng.plan_begin(START, goal, mode, mass, exec_time, max_nodes=n_samples + 1,
-                        max_batch=batch, seed=seed)
+                        max_batch=-(-batch // world), seed=seed)
     if st != _lib.PLAN_OK:
         raise RuntimeError("start/goal in collision")
-    eng.plan_run(n_samples, batch)
+    if shared is not None:
+        eng.plan_run_shared(shared, n_samples, batch)
+    else:
+        eng.plan_run(n_samples, batch)
     r = eng.plan_finish()
     out = eng.plan_fetch(r) if r.goal_found else None
     return r, out
@@ -205,6 +211,9 @@ def main():
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--self-collisions", action="store_true",
                     help="add the arm's self-collision pairs (off in the reference planner)")
+    ap.add_argument("--shared-tree", action="store_true",
+                    help="c3/c5: the GPUs grow ONE tree of the workload's samples per step "
+                         "(shared-tree rounds, strong scaling) instead of one tree per GPU")
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
@@ -223,7 +232,13 @@ def main():
         W["batch"] = args.batch
     if args.obstacles is not None:
         W["boxes"] = args.obstacles
-    if args.workload == "c5":
+    shared = args.shared_tree and W["queries"] == 1
+    if shared:
+        W["scaling"] = "strong"
+        W["text"] = W["text"].split(" -- ")[0].split(", one query per GPU")[0] + \
+            " -- shared tree: the GPUs grow one tree per step together (each rank takes its " \
+            "share of every round's lanes; goal lane, counts and new nodes exchanged over RCCL)"
+    elif args.workload == "c5":
         W["samples"] = W["samples"] // world  # 1e7 per step over all GPUs
     mode, mass = W["mode"], W["mass"]
     n_obs_total = W["boxes"] + W["meshes"]
@@ -250,7 +265,8 @@ def main():
         if comm is not None:
             comm.barrier()
 
-    step_seed = lambda s: 1234 + rank * 100003 + s  # noqa: E731
+    # a shared tree needs the same seed on every rank (one Philox stream, split by lanes)
+    step_seed = (lambda s: 1234 + s) if shared else (lambda s: 1234 + rank * 100003 + s)  # noqa: E731
 
     # several queries per rank (c4): independent queries run concurrently on separate engines
     # (handles, one HIP stream each) from host threads -- the C-ABI calls release the GIL and
@@ -271,13 +287,14 @@ def main():
             for j in range(k, len(queries), n_streams):
                 obs, pack, goal = queries[j]
                 got.append((j,) + run_query(engines[k], obs, goal, W["samples"], W["batch"],
-                                            step_seed(s) + 7919 * j, mode, mass, meshes=pack))
+                                            step_seed(s) + 7919 * j, mode, mass, meshes=pack,
+                                            shared=comm if shared else None))
             return got
         done = sorted(sum(pool.map(lane, range(n_streams)) if pool else [lane(0)], []),
                       key=lambda x: x[0])
         outs = [d[2] for d in done]
         res = [d[1].as_dict() for d in done]
-        if comm is not None:
+        if comm is not None and not shared:
             # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
             shard.gather_trajectories(comm, [shard.pack_trajectory(o) for o in outs], labels)
         return res
@@ -297,7 +314,7 @@ def main():
     if comm is not None:
         dt = float(comm.allreduce([dt], _lib.REDUCE_MAX)[0])
         total_samples = float(comm.allreduce([total_samples], _lib.REDUCE_SUM)[0])
-    n_queries_total = W["queries"] if W["queries"] > 1 else world
+    n_queries_total = W["queries"] if W["queries"] > 1 else (1 if shared else world)
     S = args.steps
     kernel_ms = {k: sum(x[k] for x in results) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
@@ -340,7 +357,8 @@ def main():
     # north-star HBM figure: compulsory bytes per query = 68 T_r per round (tree read
     # once) + 72 B_r per round (candidates written) + trajectory rows, over the step time
     snap = sum(x["snap_sum"] for x in results)
-    hbm_bytes = 68 * snap + 72 * W["samples"] * len(results) + 22 * 8 * sum(x["n_traj"] for x in results)
+    hbm_bytes = 68 * snap + 72 * sum(x["n_samples"] for x in results) + \
+        22 * 8 * sum(x["n_traj"] for x in results)
     hbm_gbs = hbm_bytes / (dt / 1.0) / 1e9 * world if dt > 0 else 0.0
 
     line = {
@@ -360,7 +378,8 @@ def main():
         "config": {"workload": W["text"], "boxes": W["boxes"], "meshes": W["meshes"],
                    "samples_per_query": W["samples"], "queries_per_step": n_queries_total,
                    "batch_per_round": W["batch"], "execution_time_s": 5.0,
-                   "parallelism": "query-sharded x%d" % world, "streams_per_gpu": n_streams,
+                   "parallelism": ("shared-tree x%d" if shared else "query-sharded x%d") % world,
+                   "streams_per_gpu": n_streams,
                    "self_collisions": bool(args.self_collisions)},
         "roofline": dominant,
         "roofline_other": other,

@@ -19,6 +19,7 @@ extern "C" {
 #endif
 
 typedef struct tcmp_handle tcmp_handle;
+typedef struct tcmp_comm tcmp_comm;  /* multi-GPU communicator (tcmp_dist_init, below) */
 
 /* torque_test modes, panda_primitives.py:228-236 */
 #define TCMP_TORQUE_BASE 0 /* get_torque_limits_not_exceded_test_base   panda_primitives.py:13 */
@@ -203,6 +204,25 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
 int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
                     int32_t* goal_found);
 
+/* shared-tree rounds (SURVEY 8e's alternative to replica trees): every rank of `c` has the
+ * same open plan (tcmp_plan_begin with identical cfg; max_nodes for the whole tree,
+ * max_batch >= ceil(batch / world)) and calls this with the same n_samples / batch; rank r
+ * takes lanes [r B / W, (r + 1) B / W) of each round of B and the ranks exchange, per round,
+ * the goal lane and the accepted-edge counts (RCCL all-reduce / all-gather on the engine
+ * stream) and then their new node records (one group of in-place ncclBroadcast calls), so
+ * every rank holds the tree a single engine builds with tcmp_plan_run(h, n_samples, batch).
+ * World 1 is tcmp_plan_run. */
+int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_t batch);
+
+/* the same rounds driven by one process over n engines (devices may repeat), the exchanges
+ * done through host copies and device-to-device copies: the single-process form of
+ * tcmp_plan_run_shared (and its parity check on one GPU). */
+int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch);
+
+/* goal node of the open plan (-1 while none) and its cost -- goal_n.cost, the bound of the
+ * informed rejection test (rrt_star.py:163-165); cost may be NULL. */
+int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost);
+
 /* device-sampled rounds of `batch` lanes until n_samples samples were drawn. */
 int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch);
 
@@ -234,7 +254,6 @@ int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn
 #define TCMP_TRAJ_COLS 22
 #define TCMP_REDUCE_SUM 0
 #define TCMP_REDUCE_MAX 1
-typedef struct tcmp_comm tcmp_comm;
 
 /* TCP rendezvous: rank 0 listens on addr:port and sends its nbytes `blob` to every other
  * rank (which connect, retrying until timeout_ms).  Host only, no GPU.  Used for the

@@ -25,6 +25,7 @@ class RrtCfg(ctypes.Structure):
         ("replay_random", _dp), ("n_replay_random", ctypes.c_long),
         ("replay_uniform", _dp), ("n_replay_uniform", ctypes.c_long),
         ("obs", _dp), ("n_obs", ctypes.c_int), ("cull", ctypes.c_int), ("validate", ctypes.c_int),
+        ("informed", ctypes.c_int),
     ]
 
 
@@ -251,7 +252,7 @@ def philox_uniforms(seed, k):
 def rrt_run(start, goal, max_samples, obs=None, torque_mode=0, mass=0.0, exec_time=5.0,
             batch=1, seed=0, replay_random=None, replay_uniform=None, radius=0.01,
             goal_prob=0.2, goal_tol=1e-2, cull=1, validate=True, cap_wp=1 << 16,
-            cap_traj=1 << 20):
+            cap_traj=1 << 20, informed=False):
     """Runs the restated RRT*; returns dict with status, counters, waypoints, traj."""
     cfg = RrtCfg()
     cfg.start[:] = list(map(float, start)); cfg.goal[:] = list(map(float, goal))
@@ -268,6 +269,9 @@ def rrt_run(start, goal, max_samples, obs=None, torque_mode=0, mass=0.0, exec_ti
     o = obstacles_array(obs); keep.append(o)
     cfg.obs = _d(o) if len(o) else None
     cfg.n_obs = len(o); cfg.cull = int(cull); cfg.validate = int(bool(validate))
+    if informed and not (replay_uniform is not None and int(batch) == 1):
+        raise ValueError("informed is restated for the replayed B = 1 loop only")
+    cfg.informed = int(bool(informed))
     res = RrtResult()
     wp = np.zeros((cap_wp, 7))
     tq = np.zeros((cap_traj, 7)); tqd = np.zeros_like(tq); tqdd = np.zeros_like(tq)

@@ -1076,6 +1076,8 @@ typedef struct {
   const double* obs; int n_obs;
   int cull;
   int validate;
+  int informed; /* rrt_star.py:163-165 (replay / B = 1): reject draws that cannot beat the
+                   goal's cost; a rejected draw is not an iteration */
 } orc_rrt_cfg;
 
 typedef struct {
@@ -1169,9 +1171,17 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
         dog[j] = dg;
         if (dg) memcpy(S + 7 * j, cfg->goal, sizeof(double) * 7);
         else {
-          if (ru >= cfg->n_replay_uniform) { res->status = 5; goto done; }
-          const double* u = cfg->replay_uniform + 7 * ru++;
-          for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];
+          for (;;) {
+            if (ru >= cfg->n_replay_uniform) { res->status = 5; goto done; }
+            const double* u = cfg->replay_uniform + 7 * ru++;
+            for (int d = 0; d < 7; ++d) S[7 * j + d] = (1 - u[d]) * ORC_LO[d] + u[d] * ORC_HI[d];
+            /* informed RRT* (rrt_star.py:163-165): distance(start, s) + distance(s, goal) >=
+             * goal_n.cost draws again without counting an iteration */
+            if (!(cfg->informed && goal_found &&
+                  orc_dist(cfg->start, S + 7 * j, C.w) + orc_dist(S + 7 * j, cfg->goal, C.w) >=
+                      T.cost[goal_n]))
+              break;
+          }
         }
       } else {
         /* batched goal bias: a lane whose draw selects the goal becomes the round's goal

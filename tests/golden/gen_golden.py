@@ -256,7 +256,7 @@ def boxes_scene(rng, n, avoid):
 
 
 def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, stride=1,
-                  want_found=None):
+                  want_found=None, informed=False):
     problem = Problem(mass, exec_time, mode)
     torque_fn = TESTS[mode](problem)
     collision_fn = make_collision_fn(obs)
@@ -272,7 +272,7 @@ def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, st
     try:
         path, vels, accels, psg = ref_rrt.rrt_star_force_aware(
             tuple(start), tuple(goal), distance_fn, sample, extend_fn, collision_fn, torque_fn,
-            dynam_fn, radius=[0.01], max_time=50, max_iterations=iters)
+            dynam_fn, radius=[0.01], max_time=50, max_iterations=iters, informed=informed)
     finally:
         ref_rrt.random = saved
     dt = time.time() - t0
@@ -284,7 +284,8 @@ def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, st
                iters=np.array(iters), seed=np.array(seed),
                replay_random=np.array(rnd.vals, dtype=np.float64),
                replay_uniform=np.array(sample.u, dtype=np.float64).reshape(-1, 7),
-               found=np.array(path is not None), stride=np.array(stride))
+               found=np.array(path is not None), stride=np.array(stride),
+               informed=np.array(bool(informed)))
     if wp_rec:
         res["waypoints"] = wp_rec[-1]
     if path is not None:
@@ -349,7 +350,19 @@ def gen_c1k():
                   [], "base", 0.0, 5.0, 1000, 0, stride=37)
 
 
+def gen_informed():
+    """informed=True (rrt_star.py:163-165; the reference planner never sets it): the empty-scene
+    rne query of rrt_empty_rne5.npz, run on past the goal so that draws that cannot beat the
+    goal's cost are rejected (they consume the sample stream but not the iteration budget)."""
+    z = np.load(os.path.join(HERE, "rrt_empty_rne5.npz"))
+    run_reference("empty_rne5_informed", z["start"], z["goal"], [], "rne", 5.0, 1.0,
+                  2 * int(z["iters"]), int(z["seed"]), stride=7, want_found=True, informed=True)
+
+
 def main():
+    if "--only-informed" in sys.argv:
+        gen_informed()
+        return
     if "--only-fk" in sys.argv:
         gen_fk(os.path.join(HERE, "fk_golden.npz"))
         return
@@ -373,6 +386,7 @@ def main():
     search("box8_base", rng, 8, "base", 0.0, 0.5, 300, 5)
     # the goal is never reached within the budget
     search("box16_rne5_short", rng, 16, "rne", 5.0, 1.0, 4, 6, want_found=False)
+    gen_informed()
 
 
 if __name__ == "__main__":

@@ -214,7 +214,8 @@ def test_rrt_golden_drop_in(eng, path, variant):
     np.random.seed(seed)
     path_, vels, accels, psg = rrt_star_force_aware(
         tuple(z["start"]), tuple(z["goal"]), dist, sample, ext, coll, torque_fn, dyn,
-        radius=[0.01], max_time=50, max_iterations=int(z["iters"]))
+        radius=[0.01], max_time=50, max_iterations=int(z["iters"]),
+        informed=bool(z["informed"]) if "informed" in z else False)
     assert (path_ is not None) == bool(z["found"])
     if path_ is None:
         return

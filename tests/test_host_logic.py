@@ -118,7 +118,8 @@ def test_host_loop_reproduces_reference(path):
     p, v, a, psg = RS.rrt_star_force_aware(tuple(z["start"]), tuple(z["goal"]), dist, sample, ext,
                                            coll, torque, _numpy_dynam_fn(float(z["exec_time"])),
                                            radius=[0.01], max_time=50,
-                                           max_iterations=int(z["iters"]))
+                                           max_iterations=int(z["iters"]),
+                                           informed=bool(z["informed"]) if "informed" in z else False)
     assert (p is not None) == bool(z["found"])
     if p is None:
         return

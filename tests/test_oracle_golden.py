@@ -47,7 +47,8 @@ def test_rrt_replay_matches_reference(path):
     rr = z["replay_random"] if len(z["replay_random"]) else np.zeros(0)
     ru = z["replay_uniform"] if len(z["replay_uniform"]) else np.zeros((0, 7))
     r = O.rrt_run(z["start"], z["goal"], int(z["iters"]), z["obs"], int(z["mode"]),
-                  float(z["mass"]), float(z["exec_time"]), replay_random=rr, replay_uniform=ru)
+                  float(z["mass"]), float(z["exec_time"]), replay_random=rr, replay_uniform=ru,
+                  informed=bool(z["informed"]) if "informed" in z else False)
     found = bool(z["found"])
     assert (r["status"] == 0) == found
     if not found:

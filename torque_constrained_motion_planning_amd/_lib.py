@@ -26,7 +26,8 @@ EXPORTS = [
     "tcmp_synchronize",
     "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
-    "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_run", "tcmp_plan_finish",
+    "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
+    "tcmp_plan_run_shared", "tcmp_plan_run_group",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
@@ -114,6 +115,10 @@ def load_library(path=LIB_PATH):
                                          ctypes.c_double, _i64p, _dp]
         L.tcmp_plan_begin.argtypes = [vp, ctypes.POINTER(PlanCfg), ctypes.POINTER(PlanResult)]
         L.tcmp_plan_round.argtypes = [vp, _dp, _u8p, ctypes.c_int32, _i32p]
+        L.tcmp_plan_goal.argtypes = [vp, _i64p, _dp]
+        L.tcmp_plan_run_shared.argtypes = [vp, vp, ctypes.c_int64, ctypes.c_int32]
+        L.tcmp_plan_run_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.c_int64,
+                                          ctypes.c_int32]
         L.tcmp_plan_run.argtypes = [vp, ctypes.c_int64, ctypes.c_int32]
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
@@ -355,6 +360,19 @@ class Engine:
                                                ctypes.byref(gf) if sync else None))
         return bool(gf.value)
 
+    def plan_run_shared(self, comm, n_samples, batch):
+        """Shared-tree rounds over the ranks of `comm` (tcmp_plan_run_shared): this rank takes
+        its share of every round's `batch` lanes; afterwards every rank holds the whole tree."""
+        self._check(self.L.tcmp_plan_run_shared(self.h, comm.h if comm is not None else None,
+                                                int(n_samples), int(batch)))
+
+    def plan_goal(self):
+        """(goal node index or -1, its cost) of the open plan."""
+        node = ctypes.c_int64(-1)
+        cost = ctypes.c_double(0.0)
+        self._check(self.L.tcmp_plan_goal(self.h, ctypes.byref(node), ctypes.byref(cost)))
+        return node.value, cost.value
+
     def plan_run(self, n_samples, batch):
         self._check(self.L.tcmp_plan_run(self.h, int(n_samples), int(batch)))
 
@@ -461,6 +479,18 @@ def rendezvous(rank, world, addr, port, blob, timeout_ms=60000):
 
 
 _engines = {}
+
+
+def plan_run_group(engines, n_samples, batch):
+    """tcmp_plan_run_group: one process drives the shared-tree rounds of several engines (the
+    same open plan on each); every engine ends with the tree one engine builds with
+    plan_run(n_samples, batch)."""
+    engines = list(engines)
+    arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+    L = load_library()
+    rc = L.tcmp_plan_run_group(arr, len(engines), int(n_samples), int(batch))
+    if rc != 0:
+        raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
 
 
 def engine(device=0):

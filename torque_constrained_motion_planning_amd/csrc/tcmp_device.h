@@ -407,9 +407,10 @@ __device__ __forceinline__ bool torque_ok(const double cq[7], const double sq[7]
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ int lane_id() { return __lane_id(); }
 
-// Wave reductions: two quad_perm and two row_ror DPP steps reduce each 16-lane row inside
-// the VALU, then four readlanes combine the rows -- no LDS round trips (ds_bpermute).  The
-// result is wave-uniform.  Call with every lane of the wave active.
+// Wave reductions, all in DPP (no LDS round trips, one readlane): two quad_perm and two row_ror
+// steps reduce each 16-lane row, row_bcast:15 folds rows 0 -> 1 and 2 -> 3, row_bcast:31 folds
+// row 1 -> rows 2 and 3 (lanes outside a broadcast's row mask keep their value through `old`),
+// so lane 63 holds the result.  Wave-uniform.  Call with every lane of the wave active.
 template <int C>
 __device__ __forceinline__ int dpp_i(int v) {
   return __builtin_amdgcn_update_dpp(0, v, C, 0xF, 0xF, true);
@@ -421,6 +422,20 @@ __device__ __forceinline__ float dpp_f(float v) {
 template <int C>
 __device__ __forceinline__ double dpp_d(double v) {
   return __hiloint2double(dpp_i<C>(__double2hiint(v)), dpp_i<C>(__double2loint(v)));
+}
+__device__ __forceinline__ int bc15_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false);
+}
+__device__ __forceinline__ int bc31_i(int v) {
+  return __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false);
+}
+__device__ __forceinline__ float bc15_f(float v) { return __int_as_float(bc15_i(__float_as_int(v))); }
+__device__ __forceinline__ float bc31_f(float v) { return __int_as_float(bc31_i(__float_as_int(v))); }
+__device__ __forceinline__ double bc15_d(double v) {
+  return __hiloint2double(bc15_i(__double2hiint(v)), bc15_i(__double2loint(v)));
+}
+__device__ __forceinline__ double bc31_d(double v) {
+  return __hiloint2double(bc31_i(__double2hiint(v)), bc31_i(__double2loint(v)));
 }
 __device__ __forceinline__ float readlane_f(float v, int l) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
@@ -434,22 +449,39 @@ __device__ __forceinline__ double wave_min(double x) {
   x = fmin(x, dpp_d<0x4E>(x));
   x = fmin(x, dpp_d<0x124>(x));
   x = fmin(x, dpp_d<0x128>(x));
+#ifdef TCMP_RED_READLANE
   return fmin(fmin(readlane_d(x, 0), readlane_d(x, 16)), fmin(readlane_d(x, 32), readlane_d(x, 48)));
+#else
+  x = fmin(x, bc15_d(x));
+  x = fmin(x, bc31_d(x));
+  return readlane_d(x, 63);
+#endif
 }
 __device__ __forceinline__ double wave_max(double x) {
   x = fmax(x, dpp_d<0xB1>(x));
   x = fmax(x, dpp_d<0x4E>(x));
   x = fmax(x, dpp_d<0x124>(x));
   x = fmax(x, dpp_d<0x128>(x));
+#ifdef TCMP_RED_READLANE
   return fmax(fmax(readlane_d(x, 0), readlane_d(x, 16)), fmax(readlane_d(x, 32), readlane_d(x, 48)));
+#else
+  x = fmax(x, bc15_d(x));
+  x = fmax(x, bc31_d(x));
+  return readlane_d(x, 63);
+#endif
 }
 __device__ __forceinline__ int wave_min_int(int x) {
   x = min(x, dpp_i<0xB1>(x));
   x = min(x, dpp_i<0x4E>(x));
   x = min(x, dpp_i<0x124>(x));
   x = min(x, dpp_i<0x128>(x));
-  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)),
-             min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+#ifdef TCMP_RED_READLANE
+  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)), min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
+#else
+  x = min(x, bc15_i(x));
+  x = min(x, bc31_i(x));
+  return __builtin_amdgcn_readlane(x, 63);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -565,20 +597,21 @@ __device__ __forceinline__ float wave_minf(float x) {
   x = fminf(x, dpp_f<0x4E>(x));
   x = fminf(x, dpp_f<0x124>(x));
   x = fminf(x, dpp_f<0x128>(x));
+#ifdef TCMP_RED_READLANE
   return fminf(fminf(readlane_f(x, 0), readlane_f(x, 16)), fminf(readlane_f(x, 32), readlane_f(x, 48)));
+#else
+  x = fminf(x, bc15_f(x));
+  x = fminf(x, bc31_f(x));
+  return readlane_f(x, 63);
+#endif
 }
-// the same minimum with the cross-row steps in DPP as well: row_bcast:15 folds rows 0 -> 1 and
-// 2 -> 3, row_bcast:31 folds row 1 -> rows 2 and 3, so lane 63 holds the wave minimum and one
-// readlane returns it (the rows' disabled lanes keep their own value through `old`)
 __device__ __forceinline__ float wave_minf_bc(float x) {
   x = fminf(x, dpp_f<0xB1>(x));
   x = fminf(x, dpp_f<0x4E>(x));
   x = fminf(x, dpp_f<0x124>(x));
   x = fminf(x, dpp_f<0x128>(x));
-  x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
-                                                          0x142, 0xA, 0xF, false)));
-  x = fminf(x, __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x),
-                                                          0x143, 0xC, 0xF, false)));
+  x = fminf(x, bc15_f(x));
+  x = fminf(x, bc31_f(x));
   return readlane_f(x, 63);
 }
 __device__ __forceinline__ float wave_maxf(float x) {
@@ -586,7 +619,13 @@ __device__ __forceinline__ float wave_maxf(float x) {
   x = fmaxf(x, dpp_f<0x4E>(x));
   x = fmaxf(x, dpp_f<0x124>(x));
   x = fmaxf(x, dpp_f<0x128>(x));
+#ifdef TCMP_RED_READLANE
   return fmaxf(fmaxf(readlane_f(x, 0), readlane_f(x, 16)), fmaxf(readlane_f(x, 32), readlane_f(x, 48)));
+#else
+  x = fmaxf(x, bc15_f(x));
+  x = fmaxf(x, bc31_f(x));
+  return readlane_f(x, 63);
+#endif
 }
 
 // fp32 first pass of exact_pd_wave on the LDS geometry.  Same candidate axes and the same

@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "../../include/tcmp.h"
+#include "tcmp_dist_internal.h"
 
 // tcmp_engine.hip's thread-local error string
 extern "C" const char* tcmp_last_error(void);
@@ -101,6 +102,46 @@ struct tcmp_comm {
     return 0;
   }
 };
+
+namespace tcmp_dist {
+
+int rank(const tcmp_comm* c) { return c->rank; }
+int world(const tcmp_comm* c) { return c->world; }
+int device(const tcmp_comm* c) { return c->device; }
+
+int allreduce_min_i64(tcmp_comm* c, int64_t* d, int n, hipStream_t s) {
+  if (c->world == 1 || n <= 0) return 0;
+  NCCLD(ncclAllReduce(d, d, (size_t)n, ncclInt64, ncclMin, c->nccl, s));
+  return 0;
+}
+
+int allgather_i64(tcmp_comm* c, const int64_t* send, int64_t* recv, int n, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (c->world == 1) {
+    HIPD(hipMemcpyAsync(recv, send, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
+    return 0;
+  }
+  NCCLD(ncclAllGather(send, recv, (size_t)n, ncclInt64, c->nccl, s));
+  return 0;
+}
+
+int bcast_group(tcmp_comm* c, const Bcast* ops, int n_ops, hipStream_t s) {
+  if (c->world == 1 || n_ops <= 0) return 0;
+  NCCLD(ncclGroupStart());
+  for (int i = 0; i < n_ops; ++i) {
+    if (ops[i].bytes == 0) continue;
+    const ncclResult_t r = ncclBroadcast(ops[i].ptr, ops[i].ptr, ops[i].bytes, ncclUint8,
+                                         ops[i].root, c->nccl, s);
+    if (r != ncclSuccess) {
+      (void)ncclGroupEnd();
+      return fail(-5, std::string("ncclBroadcast: ") + ncclGetErrorString(r));
+    }
+  }
+  NCCLD(ncclGroupEnd());
+  return 0;
+}
+
+}  // namespace tcmp_dist
 
 extern "C" {
 

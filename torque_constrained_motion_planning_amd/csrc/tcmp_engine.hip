@@ -30,6 +30,7 @@
 
 #include "tcmp_device.h"
 #include "../../include/tcmp.h"
+#include "tcmp_dist_internal.h"
 
 using namespace tcmp;
 
@@ -72,7 +73,10 @@ struct DevState {
   unsigned long long nn_box_tests;
   unsigned long long snap_sum;       // sum over rounds of the snapshot size T_r
   unsigned long long nn_full_pairs;  // sum over rounds of T_r * B_r (brute-force-equivalent)
-  long long ins_total;   // accepted edges of the current round (k_ins_scan)
+  long long ins_total;   // accepted edges of the current round (k_ins_scan), this engine's lanes
+  long long ins_off;     // where this engine's new nodes start after the snapshot (0 alone;
+                         // the lower ranks' accepted edges in a shared-tree round)
+  long long ins_all;     // accepted edges of the round over all ranks (ins_total alone)
   long long ins_goal;    // lowest goal-reaching new node of the round (k_ins_write)
   int work_counter;
   int nn_counter;
@@ -863,6 +867,8 @@ struct tcmp_handle {
   DBuf<unsigned char> sort_tmp;
   DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
   int nn_waves_per_cu = 16;
+  hipEvent_t ins_ev = nullptr;     // open F_INSERT mark between round_search and round_finish
+  DBuf<long long> xch;             // shared-tree round exchange slots (k_sr_*)
   int nn_cand_bits = 16;           // top key bits the candidates are sorted by
   DBuf<double> second;
   DBuf<long long> chain;
@@ -2066,9 +2072,16 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
   return x;
 }
 
-static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t* is_goal,
-                           int32_t nb) {
-  const PlanParams& P = h->P;
+// ---- one round, in phases.  A lone engine runs them back to back (plan_round_impl); the
+// engines of a shared-tree round (tcmp_plan_run_shared / tcmp_plan_run_group) each own a
+// consecutive range of the round's lanes and exchange four small things between the phases:
+// the round's goal lane, their accepted-edge counts, the lowest goal-reaching new node, and
+// finally their new node records -- so every engine ends the round with the tree a lone
+// engine would have built from the whole round.
+//
+// sample: the host's draws (samples != NULL), or Philox lanes [lo, lo + nb) of a round of B
+static int round_sample(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
+                        long long lo, long long B) {
   if (samples) {
     std::vector<double> tmp((size_t)nb * 8, 0.0);
     double cmax = 0.0;
@@ -2094,21 +2107,26 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
     HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
   } else {
     hipLaunchKernelGGL(k_sample, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
-                       (long long)h->samples_issued, nb, h->cand.p, h->cgoal.p);
+                       (long long)h->samples_issued + lo, nb, h->cand.p, h->cgoal.p);
     HIPCHK(hipGetLastError());
   }
-  h->samples_issued += nb;
-  Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
+  h->samples_issued += B;
+  return 0;
+}
+
+// goal lane fix, nearest, extend (edge kernel), and the count/scan half of the insertion
+static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long long B) {
+  const PlanParams& P = h->P;
   hipEvent_t e0;
   h->mark_begin(F_NEAREST, &e0);
-  if (!samples) {
+  if (device_samples) {
     hipLaunchKernelGGL(k_goal_fix, dim3(1), dim3(64), 0, h->stream, h->dP, h->st, h->cand.p,
                        h->cgoal.p, nb);
     HIPCHK(hipGetLastError());
   }
   // the snapshot holds at most 1 + (samples issued before this round) nodes
   {
-    const long long T_bound = 1 + h->samples_issued - nb;
+    const long long T_bound = 1 + h->samples_issued - B;
     if (int rc = launch_nearest(h, P, h->dP, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
                                 h->second.p, h->nnscore.p))
       return rc;
@@ -2132,7 +2150,7 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   }
   if (int rc = launch_edges(h, J, h->dP, false)) return rc;
   h->mark_end(F_EDGES, e0);
-  h->mark_begin(F_INSERT, &e0);
+  h->mark_begin(F_INSERT, &h->ins_ev);
   {
     const int nblk = (int)grid_for(nb, 256);
     if (int rc = h->bcount.ensure(nblk)) return rc;
@@ -2141,13 +2159,29 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
                        h->bcount.p);
     hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
                        h->boff.p);
-    hipLaunchKernelGGL(k_ins_write, dim3(nblk), dim3(256), 0, h->stream, h->dP, h->st, tr, h->nn.p,
-                       h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->boff.p,
-                       h->second.p, h->rwlist.p);
-    hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, h->dP, h->st, nb);
     HIPCHK(hipGetLastError());
   }
-  h->mark_end(F_INSERT, e0);
+  return 0;
+}
+
+// the new nodes, in lane order after the snapshot (and after the lower ranks' new nodes)
+static int round_write(tcmp_handle* h, int32_t nb) {
+  Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
+  const int nblk = (int)grid_for(nb, 256);
+  hipLaunchKernelGGL(k_ins_write, dim3(nblk), dim3(256), 0, h->stream, h->dP, h->st, tr, h->nn.p,
+                     h->cand.p, h->cgoal.p, h->nsafe.p, h->nsteps.p, h->last.p, nb, h->boff.p,
+                     h->second.p, h->rwlist.p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+// node count / goal bookkeeping, then the rewire of this engine's new nodes
+static int round_finish(tcmp_handle* h, int32_t nb) {
+  Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
+  hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, h->dP, h->st, nb);
+  HIPCHK(hipGetLastError());
+  h->mark_end(F_INSERT, h->ins_ev);
+  hipEvent_t e0;
   h->mark_begin(F_REWIRE, &e0);
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
@@ -2159,6 +2193,56 @@ static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t*
   return 0;
 }
 
+static int plan_round_impl(tcmp_handle* h, const double* samples, const uint8_t* is_goal,
+                           int32_t nb) {
+  if (int rc = round_sample(h, samples, is_goal, nb, 0, nb)) return rc;
+  if (int rc = round_search(h, samples == nullptr, nb, nb)) return rc;
+  if (int rc = round_write(h, nb)) return rc;
+  return round_finish(h, nb);
+}
+
+// ---- shared-tree rounds: the exchanges ------------------------------------------------------
+// xch (int64, per engine): [0] the round's goal lane (global lane index, LLONG_MAX for none),
+// [1] this engine's accepted edges, [2] the lowest goal-reaching new node, [3 + q] engine q's
+// accepted edges (gathered).
+__global__ void k_sr_put_lane(DevState* st, long long lo, long long* xch) {
+  xch[0] = st->round_goal == INT_MAX ? LLONG_MAX : lo + (long long)st->round_goal;
+}
+__global__ void k_sr_take_lane(DevState* st, long long lo, int nb, const long long* xch) {
+  const long long g = xch[0];
+  st->round_goal = (g >= lo && g < lo + nb) ? (int)(g - lo) : INT_MAX;
+}
+__global__ void k_sr_put_count(const DevState* st, long long* xch) { xch[1] = st->ins_total; }
+__global__ void k_sr_take_counts(DevState* st, int rank, int world, const long long* xch) {
+  long long off = 0, all = 0;
+  for (int q = 0; q < world; ++q) {
+    if (q < rank) off += xch[3 + q];
+    all += xch[3 + q];
+  }
+  st->ins_off = off;
+  st->ins_all = all;
+}
+__global__ void k_sr_put_goal(const DevState* st, long long* xch) { xch[2] = st->ins_goal; }
+__global__ void k_sr_take_goal(DevState* st, const long long* xch) { st->ins_goal = xch[2]; }
+
+// lanes of engine q in a round of B lanes over W engines
+static inline long long sr_lo(long long B, int q, int W) { return B * q / W; }
+
+// a host-side copy of the tree size, advanced like k_ins_final does
+static int sr_tree_size(tcmp_handle* h, long long* T) {
+  HIPCHK(hipMemcpyAsync(T, &h->st->n_nodes, sizeof(*T), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+static int sr_check(tcmp_handle* h, long long n_samples, int batch, int world) {
+  if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
+  if (batch < world) return fail(-1, "a shared-tree round needs at least one lane per engine");
+  if ((batch + world - 1) / world > h->max_batch)
+    return fail(-1, "batch / engines exceeds the plan's max_batch");
+  if (h->samples_issued + n_samples + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
+  return h->xch.ensure(3 + (size_t)world);
+}
 int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
                     int32_t* goal_found) {
   if (int rc = set_dev(h)) return rc;
@@ -2171,6 +2255,192 @@ int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goa
     HIPCHK(hipMemcpyAsync(&g, &h->st->goal_node, sizeof(g), hipMemcpyDeviceToHost, h->stream));
     HIPCHK(hipStreamSynchronize(h->stream));
     *goal_found = g >= 0;
+  }
+  return 0;
+}
+
+int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_t batch) {
+  if (int rc = set_dev(h)) return rc;
+  if (!c) return fail(-1, "null comm");
+  const int W = tcmp_dist::world(c), r = tcmp_dist::rank(c);
+  if (W == 1) return tcmp_plan_run(h, n_samples, batch);
+  if (int rc = sr_check(h, n_samples, batch, W)) return rc;
+  long long T = 0;
+  if (int rc = sr_tree_size(h, &T)) return rc;
+  std::vector<long long> cnt((size_t)W, 0);
+  long long* x = h->xch.p;
+  for (long long left = n_samples; left > 0;) {
+    const long long B = std::min<long long>(left, batch);
+    const long long lo = sr_lo(B, r, W);
+    const int nb = (int)(sr_lo(B, r + 1, W) - lo);
+    if (int rc = round_sample(h, nullptr, nullptr, nb, lo, B)) return rc;
+    // the round's goal lane: the lowest selecting lane of the whole round (k_sample's rule)
+    hipLaunchKernelGGL(k_sr_put_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo, x);
+    if (int rc = tcmp_dist::allreduce_min_i64(c, reinterpret_cast<int64_t*>(x), 1, h->stream)) return rc;
+    hipLaunchKernelGGL(k_sr_take_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo, nb, x);
+    if (int rc = round_search(h, true, nb, B)) return rc;
+    // accepted edges of every rank: this rank's insertion offset and the round's total
+    hipLaunchKernelGGL(k_sr_put_count, dim3(1), dim3(1), 0, h->stream, h->st, x);
+    if (int rc = tcmp_dist::allgather_i64(c, reinterpret_cast<const int64_t*>(x + 1),
+                                         reinterpret_cast<int64_t*>(x + 3), 1, h->stream))
+      return rc;
+    hipLaunchKernelGGL(k_sr_take_counts, dim3(1), dim3(1), 0, h->stream, h->st, r, W, x);
+    HIPCHK(hipMemcpyAsync(cnt.data(), x + 3, W * sizeof(long long), hipMemcpyDeviceToHost,
+                          h->stream));
+    if (int rc = round_write(h, nb)) return rc;
+    // the lowest goal-reaching new node of the round
+    hipLaunchKernelGGL(k_sr_put_goal, dim3(1), dim3(1), 0, h->stream, h->st, x);
+    if (int rc = tcmp_dist::allreduce_min_i64(c, reinterpret_cast<int64_t*>(x + 2), 1, h->stream))
+      return rc;
+    hipLaunchKernelGGL(k_sr_take_goal, dim3(1), dim3(1), 0, h->stream, h->st, x);
+    if (int rc = round_finish(h, nb)) return rc;
+    HIPCHK(hipStreamSynchronize(h->stream));  // cnt
+    long long all = 0;
+    for (long long v : cnt) all += v;
+    if (T + all <= h->P.max_nodes) {
+      // every rank's new nodes (rewired) to every other rank, in place
+      std::vector<tcmp_dist::Bcast> ops;
+      long long off = T;
+      for (int q = 0; q < W; ++q) {
+        const size_t k = (size_t)cnt[q];
+        if (k) {
+          ops.push_back({h->cfg.p + 8 * (size_t)off, k * 8 * sizeof(double), q});
+          ops.push_back({h->tgt.p + 8 * (size_t)off, k * 8 * sizeof(double), q});
+          ops.push_back({h->parent.p + off, k * sizeof(int), q});
+          ops.push_back({h->meta.p + off, k * sizeof(int2), q});
+        }
+        off += cnt[q];
+      }
+      if (int rc = tcmp_dist::bcast_group(c, ops.data(), (int)ops.size(), h->stream)) return rc;
+      T += all;
+    }
+    left -= B;
+  }
+  return 0;
+}
+
+int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch) {
+  if (!hs || n < 1) return fail(-1, "bad arguments");
+  if (n == 1) return tcmp_plan_run(hs[0], n_samples, batch);
+  for (int q = 0; q < n; ++q) {
+    if (!hs[q]) return fail(-1, "null handle");
+    if (int rc = set_dev(hs[q])) return rc;
+    if (int rc = sr_check(hs[q], n_samples, batch, n)) return rc;
+    if (hs[q]->samples_issued != hs[0]->samples_issued)
+      return fail(-1, "the engines' plans are not at the same round");
+  }
+  long long T = 0;
+  if (int rc = set_dev(hs[0])) return rc;
+  if (int rc = sr_tree_size(hs[0], &T)) return rc;
+  std::vector<long long> v((size_t)n), cnt((size_t)n);
+  auto sync_all = [&]() -> int {
+    for (int q = 0; q < n; ++q) {
+      if (int rc = set_dev(hs[q])) return rc;
+      HIPCHK(hipStreamSynchronize(hs[q]->stream));
+    }
+    return 0;
+  };
+  // host-side exchange: slot `i` of every engine <- the minimum over the engines
+  auto host_min = [&](int i) -> int {
+    if (int rc = sync_all()) return rc;
+    long long m = LLONG_MAX;
+    for (int q = 0; q < n; ++q) {
+      if (int rc = set_dev(hs[q])) return rc;
+      HIPCHK(hipMemcpy(&v[q], hs[q]->xch.p + i, sizeof(long long), hipMemcpyDeviceToHost));
+      m = std::min(m, v[q]);
+    }
+    for (int q = 0; q < n; ++q) {
+      if (int rc = set_dev(hs[q])) return rc;
+      HIPCHK(hipMemcpy(hs[q]->xch.p + i, &m, sizeof(long long), hipMemcpyHostToDevice));
+    }
+    return 0;
+  };
+  for (long long left = n_samples; left > 0;) {
+    const long long B = std::min<long long>(left, batch);
+    auto lo = [&](int q) { return sr_lo(B, q, n); };
+    auto nbq = [&](int q) { return (int)(sr_lo(B, q + 1, n) - sr_lo(B, q, n)); };
+    for (int q = 0; q < n; ++q) {
+      tcmp_handle* h = hs[q];
+      if (int rc = set_dev(h)) return rc;
+      if (int rc = round_sample(h, nullptr, nullptr, nbq(q), lo(q), B)) return rc;
+      hipLaunchKernelGGL(k_sr_put_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo(q), h->xch.p);
+    }
+    if (int rc = host_min(0)) return rc;
+    for (int q = 0; q < n; ++q) {
+      tcmp_handle* h = hs[q];
+      if (int rc = set_dev(h)) return rc;
+      hipLaunchKernelGGL(k_sr_take_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo(q), nbq(q),
+                         h->xch.p);
+      if (int rc = round_search(h, true, nbq(q), B)) return rc;
+      hipLaunchKernelGGL(k_sr_put_count, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
+    }
+    if (int rc = sync_all()) return rc;
+    for (int q = 0; q < n; ++q) {
+      if (int rc = set_dev(hs[q])) return rc;
+      HIPCHK(hipMemcpy(&cnt[q], hs[q]->xch.p + 1, sizeof(long long), hipMemcpyDeviceToHost));
+    }
+    for (int q = 0; q < n; ++q) {
+      tcmp_handle* h = hs[q];
+      if (int rc = set_dev(h)) return rc;
+      HIPCHK(hipMemcpy(h->xch.p + 3, cnt.data(), n * sizeof(long long), hipMemcpyHostToDevice));
+      hipLaunchKernelGGL(k_sr_take_counts, dim3(1), dim3(1), 0, h->stream, h->st, q, n, h->xch.p);
+      if (int rc = round_write(h, nbq(q))) return rc;
+      hipLaunchKernelGGL(k_sr_put_goal, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
+    }
+    if (int rc = host_min(2)) return rc;
+    for (int q = 0; q < n; ++q) {
+      tcmp_handle* h = hs[q];
+      if (int rc = set_dev(h)) return rc;
+      hipLaunchKernelGGL(k_sr_take_goal, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
+      if (int rc = round_finish(h, nbq(q))) return rc;
+    }
+    if (int rc = sync_all()) return rc;
+    long long all = 0;
+    for (long long c : cnt) all += c;
+    if (T + all <= hs[0]->P.max_nodes) {
+      long long off = T;
+      for (int q = 0; q < n; ++q) {
+        const size_t k = (size_t)cnt[q];
+        for (int p = 0; p < n && k; ++p) {
+          if (p == q) continue;
+          tcmp_handle* d = hs[p];
+          tcmp_handle* s = hs[q];
+          if (int rc = set_dev(d)) return rc;
+          HIPCHK(hipMemcpyAsync(d->cfg.p + 8 * off, s->cfg.p + 8 * off, k * 8 * sizeof(double),
+                                hipMemcpyDefault, d->stream));
+          HIPCHK(hipMemcpyAsync(d->tgt.p + 8 * off, s->tgt.p + 8 * off, k * 8 * sizeof(double),
+                                hipMemcpyDefault, d->stream));
+          HIPCHK(hipMemcpyAsync(d->parent.p + off, s->parent.p + off, k * sizeof(int),
+                                hipMemcpyDefault, d->stream));
+          HIPCHK(hipMemcpyAsync(d->meta.p + off, s->meta.p + off, k * sizeof(int2),
+                                hipMemcpyDefault, d->stream));
+        }
+        off += cnt[q];
+      }
+      if (int rc = sync_all()) return rc;
+      T += all;
+    }
+    left -= B;
+  }
+  return 0;
+}
+
+int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost) {
+  if (int rc = set_dev(h)) return rc;
+  if (!node) return fail(-1, "null node");
+  if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
+  long long g = -1;
+  HIPCHK(hipMemcpyAsync(&g, &h->st->goal_node, sizeof(g), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *node = g;
+  if (cost) {
+    double c = INFINITY;
+    if (g >= 0) {
+      HIPCHK(hipMemcpyAsync(&c, h->cfg.p + 8 * (size_t)g + 7, sizeof(c), hipMemcpyDeviceToHost,
+                            h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+    }
+    *cost = c;
   }
   return 0;
 }

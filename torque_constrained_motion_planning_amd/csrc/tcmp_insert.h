@@ -1,7 +1,9 @@
 // tcmp_insert.h -- lane-ordered insertion of a round's accepted edges (rrt_star.py:173-180),
 // as a device-wide scan: count per 256-lane block, one-block scan of the counts, then every
 // block writes its nodes at (snapshot size + block offset + in-block rank).  Node order is
-// therefore lane order, exactly as the single-pass reference loop appends them.
+// therefore lane order, exactly as the single-pass reference loop appends them.  In a
+// shared-tree round (tcmp_plan_run_shared) the engines own consecutive lane ranges and add
+// ins_off = the lower ranks' accepted edges, so the global order is still lane order.
 // Included by tcmp_engine.hip after the state types.
 #pragma once
 
@@ -37,6 +39,8 @@ __global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcou
   }
   if (tid == 0) {
     st->ins_total = run;
+    st->ins_off = 0;
+    st->ins_all = run;
     st->ins_goal = LLONG_MAX;
     st->rw_count = 0;
   }
@@ -50,9 +54,8 @@ __global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict_
                                                    int* rwlist) {
   const PlanParams P = *Pd;
   __shared__ int wc[4];
-  const long long T = st->n_nodes;
-  const long long total = st->ins_total;
-  if (T + total > P.max_nodes) return;  // k_ins_final flags the overflow
+  const long long T = st->n_nodes + st->ins_off;
+  if (st->n_nodes + st->ins_all > P.max_nodes) return;  // k_ins_final flags the overflow
   const bool goal_open = st->goal_node < 0;
   const int j = blockIdx.x * 256 + threadIdx.x;
   const bool v = j < nb && nsafe[j] > 0;
@@ -92,7 +95,7 @@ __global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict_
 
 __global__ void k_ins_final(const PlanParams* __restrict__ Pd, DevState* st, int nb) {
   const PlanParams P = *Pd;
-  const long long T = st->n_nodes, total = st->ins_total;
+  const long long T = st->n_nodes, total = st->ins_all;
   st->snap = T;
   if (T + total > P.max_nodes) {
     st->overflow = 1;

@@ -10,7 +10,7 @@ fn -- recognised by type):
   tcmp_plan_round (nearest / extend / collision / torque / insert / rewire on the device);
   tcmp_plan_finish does retrace + min-jerk + the final dynamic torque validation.  A foreign
   dynam_fn is applied on the host to the engine's retraced waypoints.
-* host loop -- distance or extend is foreign (or informed=True): the tree is kept as arrays
+* host loop -- distance or extend is foreign: the tree is kept as arrays
   on the host (_Tree).  Each foreign callback is called exactly where the reference calls it;
   the package's own collision / torque tests are evaluated by the engine in one batched
   launch per extend sequence (tcmp_check_configs / tcmp_torque_ok, or tcmp_check_edges for
@@ -54,9 +54,10 @@ def rrt_star_force_aware(start, goal, distance, sample, extend, collision, torqu
                          informed=False):
     """rrt_star.py:151-211 -> (path, vels, accels, psg) or (None, None, None, None)."""
     k = _kinds(distance, sample, extend, collision, torque_fn, dynam_fn)
-    if not informed and k["distance"] and k["extend"] and k["collision"] and k["torque"]:
+    if k["distance"] and k["extend"] and k["collision"] and k["torque"]:
         res, _, _ = _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn,
-                                dynam_fn, radius, max_iterations, goal_probability, k["dynam"])
+                                dynam_fn, radius, max_iterations, goal_probability, k["dynam"],
+                                informed)
         return res
     return _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn,
                      radius, max_time, max_iterations, goal_probability, informed, k)
@@ -111,7 +112,7 @@ def _finish(eng, dynam_fn=None, torque_fn=None):
 
 # ---- engine loop ---------------------------------------------------------------------------
 def _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
-                max_iterations, goal_probability, native_dynam=True):
+                max_iterations, goal_probability, native_dynam=True, informed=False):
     if max_iterations == INF:
         raise ValueError("max_iterations must be finite (the reference's time guard never "
                          "fires, rrt_star.py:159, so INF iterations never return)")
@@ -128,13 +129,22 @@ def _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn, dyn
         print("start config in collision")
         return (None, None, None, None), None, None
     goal_found = False
+    goal_cost = INF
     it = 0
     while it < max_iterations:
         # rrt_star.py:160-161: random() only while the goal is open and it > 0
         do_goal = (not goal_found) and (it == 0 or random() < goal_probability)
         s = goal if do_goal else sample()
+        # informed RRT* (rrt_star.py:163-165): goal_n.cost is fixed once its insertion round
+        # (rewiring included) is over -- only the newest node is ever rewired
+        if informed and goal_found and distance(start, s) + distance(s, goal) >= goal_cost:
+            print("greater than cost")
+            continue
         it += 1
-        goal_found = eng.plan_round(np.asarray([s], dtype=np.float64)[:, :7], [do_goal])
+        found = eng.plan_round(np.asarray([s], dtype=np.float64)[:, :7], [do_goal])
+        if found and not goal_found and informed:
+            goal_cost = eng.plan_goal()[1]
+        goal_found = found
     return _finish(eng, None if native_dynam else dynam_fn, torque_fn)
 
 
@@ -223,8 +233,8 @@ class _Tree:
 
 def _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
               max_time=INF, max_iterations=INF, goal_probability=.2, informed=False, kinds=None):
-    """rrt_star.py:151-211 with the tree on the host, for foreign distance / extend callbacks
-    (and informed=True).  Callback call order is the reference's, except that the package's
+    """rrt_star.py:151-211 with the tree on the host, for foreign distance / extend callbacks.
+    Callback call order is the reference's, except that the package's
     own collision and torque tests are evaluated for a whole extend sequence at once (they
     are pure functions, so that is unobservable)."""
     k = kinds if kinds is not None else _kinds(distance, sample, extend, collision, torque_fn,
