@@ -142,7 +142,10 @@ __global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long l
   }
   cgoal[j] = 0;
   const bool raw = st->goal_node < 0 && (it == 0 || u[7] < P.goal_prob);
-  if (raw) atomicMin(&st->round_goal, j);
+  // the round's lowest selecting lane: one atomic per wave (its lowest selecting lane -- lanes
+  // hold consecutive j), not one per selecting lane (a fifth of them while the goal is open)
+  const uint64_t m = __ballot(raw);
+  if (m && lane_id() == __builtin_ctzll(m)) atomicMin(&st->round_goal, j);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -164,7 +167,10 @@ __global__ void k_goal_fix(const PlanParams* __restrict__ Pd, DevState* st, doub
 // 2^36 cells leave at most a handful of nodes per cell, and the radix sorts run 5 digit
 // passes instead of 8.
 // ------------------------------------------------------------------------------------------
-constexpr int kKeyBits = 36;
+#ifndef TCMP_KEY_BITS
+#define TCMP_KEY_BITS 36
+#endif
+constexpr int kKeyBits = TCMP_KEY_BITS;
 // rocprim picks a block-sort + merge-sort chain (~15 launches) below 1M items by default;
 // the Onesweep radix sort (one histogram pass + one launch per 8-bit digit) is faster here
 using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
