@@ -635,6 +635,14 @@ __device__ __forceinline__ float wave_maxf(float x) {
 // few 1e-6 m for coordinates of a few metres), and only results within kExactGuard of kPen
 // are re-evaluated in fp64: the collision decision is always the fp64 one.
 constexpr float kExactGuard = 1e-4f;
+constexpr int max_link_edges() {
+  int m = 0;
+  for (int l = 0; l < TCMP_NLINKS; ++l) {
+    const int n = tcmp_geo_edge_off[l + 1] - tcmp_geo_edge_off[l];
+    m = n > m ? n : m;
+  }
+  return m;
+}
 #ifdef TCMP_PROF_EXACT
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
@@ -708,45 +716,80 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
       return lf;
     }
   }
+  // Edge axes in two passes.  Pass 1 (one edge per lane) marks the (edge, box axis) pairs
+  // whose adjacent facet normals straddle the plane normal to the axis -- a few per cent of
+  // them; pass 2 evaluates only the marked pairs, one per lane, each lane finding its pair by
+  // its rank among the marks (a wave prefix sum of the per-lane counts, then a binary search
+  // over the lanes).  The axis set is the one-pass test's, so the minimum is too.
+  static_assert(max_link_edges() <= 640, "pass-1 marks: 3 bits per 64-edge slice in 32");
   bool deg = false;
-  for (int base = e0; base < e1; base += 64) {
+  unsigned sil = 0;  // bit 3 it + i: edge e0 + 64 it + lane against box axis i
+  for (int it = 0, base = e0; base < e1; ++it, base += 64) {
     const int e = base + lane;
     if (e < e1) {
       const ushort4 ix = g.eidx[e];
-      const float ax0 = g.verts32[3 * ix.x], ay0 = g.verts32[3 * ix.x + 1], az0 = g.verts32[3 * ix.x + 2];
-      const float ex = g.verts32[3 * ix.y] - ax0, ey = g.verts32[3 * ix.y + 1] - ay0,
-                  ez = g.verts32[3 * ix.y + 2] - az0;
       const float4 n1 = g.planes32[ix.z];
       const float4 n2 = g.planes32[ix.w];
-      const float el2 = ex * ex + ey * ey + ez * ez;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
         const float a0 = A[0 + i], a1 = A[3 + i], a2 = A[6 + i];
         const float s1 = n1.x * a0 + n1.y * a1 + n1.z * a2;
         const float s2 = n2.x * a0 + n2.y * a1 + n2.z * a2;
         deg |= ((int)(fabsf(s1) < 1e-5f) | (int)(fabsf(s2) < 1e-5f)) != 0;
-        if (s1 * s2 < 0.f) {
-          float m0 = ey * a2 - ez * a1, m1 = ez * a0 - ex * a2, m2 = ex * a1 - ey * a0;
-          const float len2 = m0 * m0 + m1 * m1 + m2 * m2;
-          if (len2 < 1e-8f * el2) {
-            deg = true;
-          } else {
-            const float ori = m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z);
-            const float il = rsqrtf(len2);
-            deg |= fabsf(ori) * il < 1e-4f;
-            if (ori < 0.f) { m0 = -m0; m1 = -m1; m2 = -m2; }
-            const float hv = m0 * ax0 + m1 * ay0 + m2 * az0;
-            const float pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
-            const float rad = h[0] * fabsf(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
-                              h[1] * fabsf(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
-                              h[2] * fabsf(m0 * A[2] + m1 * A[5] + m2 * A[8]);
-            loc = fminf(loc, (hv - pc + rad) * il);
-          }
-        }
+        if (s1 * s2 < 0.f) sil |= 1u << (3 * it + i);
+      }
+    }
+  }
+  const int cnt = __builtin_popcount(sil);
+  int pre = cnt;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(pre, o);
+    if (lane >= o) pre += t;
+  }
+  const int total = __shfl(pre, 63);
+  pre -= cnt;  // exclusive prefix: lane l's marks are pairs [pre, pre + cnt)
+  for (int w0 = 0; w0 < total; w0 += 64) {
+    const int w = w0 + lane;
+    int src = 0;  // the last lane whose prefix is <= w
+#pragma unroll
+    for (int step = 32; step; step >>= 1)
+      if (__shfl(pre, src + step) <= w) src += step;
+    unsigned m = (unsigned)__shfl((int)sil, src);
+    const int k = w - __shfl(pre, src);
+    if (w < total) {
+      for (int j = 0; j < k; ++j) m &= m - 1;
+      const int bit = __builtin_ctz(m);
+      const int it = bit / 3, i = bit - 3 * it;
+      const ushort4 ix = g.eidx[e0 + 64 * it + src];
+      const float ax0 = g.verts32[3 * ix.x], ay0 = g.verts32[3 * ix.x + 1], az0 = g.verts32[3 * ix.x + 2];
+      const float ex = g.verts32[3 * ix.y] - ax0, ey = g.verts32[3 * ix.y + 1] - ay0,
+                  ez = g.verts32[3 * ix.y + 2] - az0;
+      const float4 n1 = g.planes32[ix.z];
+      const float4 n2 = g.planes32[ix.w];
+      const float el2 = ex * ex + ey * ey + ez * ez;
+      const float a0 = i == 0 ? A[0] : i == 1 ? A[1] : A[2];
+      const float a1 = i == 0 ? A[3] : i == 1 ? A[4] : A[5];
+      const float a2 = i == 0 ? A[6] : i == 1 ? A[7] : A[8];
+      float m0 = ey * a2 - ez * a1, m1 = ez * a0 - ex * a2, m2 = ex * a1 - ey * a0;
+      const float len2 = m0 * m0 + m1 * m1 + m2 * m2;
+      if (len2 < 1e-8f * el2) {
+        deg = true;
+      } else {
+        const float ori = m0 * (n1.x + n2.x) + m1 * (n1.y + n2.y) + m2 * (n1.z + n2.z);
+        const float il = rsqrtf(len2);
+        deg |= fabsf(ori) * il < 1e-4f;
+        if (ori < 0.f) { m0 = -m0; m1 = -m1; m2 = -m2; }
+        const float hv = m0 * ax0 + m1 * ay0 + m2 * az0;
+        const float pc = m0 * cl[0] + m1 * cl[1] + m2 * cl[2];
+        const float rad = h[0] * fabsf(m0 * A[0] + m1 * A[3] + m2 * A[6]) +
+                          h[1] * fabsf(m0 * A[1] + m1 * A[4] + m2 * A[7]) +
+                          h[2] * fabsf(m0 * A[2] + m1 * A[5] + m2 * A[8]);
+        loc = fminf(loc, (hv - pc + rad) * il);
       }
     }
     // early "free" once a trustworthy axis is below kPen - guard (no degenerate axis so far)
-    if (base + 64 < e1 && !__ballot(deg)) {
+    if (w0 + 64 < total && !__ballot(deg)) {
       const float lf = fminf(pd, wave_minf(loc));
       if (lf < P - kExactGuard) {
 #ifdef TCMP_PROF_EXACT
