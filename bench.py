@@ -131,22 +131,32 @@ def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None, n_me
             return obs, pack, goal
 
 
+HOST_MS = {"begin": 0.0, "run": 0.0, "finish": 0.0, "fetch": 0.0}  # host wall time per call
+
+
 def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass=5.0,
               exec_time=5.0, meshes=None, shared=None):
     """One planning query.  shared: a communicator -- the ranks then grow ONE tree together
     (tcmp_plan_run_shared: each rank takes its share of every round's lanes)."""
     eng.set_scene(obs, meshes)
     world = shared.world if shared is not None else 1
+    t0 = time.perf_counter()
     st = eng.plan_begin(START, goal, mode, mass, exec_time, max_nodes=n_samples + 1,
                         max_batch=-(-batch // world), seed=seed)
     if st != _lib.PLAN_OK:
         raise RuntimeError("start/goal in collision")
+    t1 = time.perf_counter()
     if shared is not None:
         eng.plan_run_shared(shared, n_samples, batch)
     else:
         eng.plan_run(n_samples, batch)
+    t2 = time.perf_counter()
     r = eng.plan_finish()
+    t3 = time.perf_counter()
     out = eng.plan_fetch(r) if r.goal_found else None
+    t4 = time.perf_counter()
+    for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
+        HOST_MS[k] += (b - a) * 1e3
     return r, out
 
 
@@ -303,6 +313,8 @@ def main():
         step(10_000 + w)
 
     barrier()
+    for k in HOST_MS:
+        HOST_MS[k] = 0.0
     t0 = time.perf_counter()
     results = []
     for s in range(args.steps):
@@ -320,7 +332,9 @@ def main():
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
     if args.verbose and rank == 0:
         print(json.dumps({"per_step": results, "kernel_ms_per_step": kernel_ms}), file=sys.stderr)
-    launches = sum(x["launches_nearest"] for x in results)  # one k_edges and one nearest scan per round
+    launches = sum(x["launches_nearest"] for x in results)  # one k_edges launch per round
+    # one scan per round, except a one-node first round (nearest = the root, no index)
+    scans = sum(x["launches_nn_scan"] for x in results)
 
     # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
     # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
@@ -330,12 +344,12 @@ def main():
     nn_ms = sum(x["ms_nn_scan"] for x in results)
     nn_tf = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     roof_nn = {
-        "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, launches),
+        "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, scans),
         "bound": "valu_fp32", "achieved": nn_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32", args.workload),
         "algorithmic": "%d flop per evaluated (candidate, node) pair; %d pairs over %d launches "
                        "(brute force would be %d pairs: %.1f PFLOP/s equivalent)" % (
-                           NN_FLOP_PER_PAIR, nn_pairs, launches, nn_full,
+                           NN_FLOP_PER_PAIR, nn_pairs, scans, nn_full,
                            NN_FLOP_PER_PAIR * nn_full / (nn_ms * 1e-3) / 1e15 if nn_ms else 0.0)}
     # k_edges: SURVEY 8d per-step work F_fk + F_bp * L * n_obs + F_rne, + F_sat per pair that
     # survives the cull (device counters), fp64 VALU
@@ -388,6 +402,9 @@ def main():
                          "definition": "SURVEY 8d compulsory bytes: 68 T_r + 72 B_r per round "
                                        "+ 176 B per trajectory row, whole job"},
         "kernel_ms_per_step": kernel_ms,
+        # host wall time inside the C-ABI calls (rank 0; the GPU work of a step completes
+        # inside plan_finish's first wait, so "finish" holds most of the step)
+        "host_ms_per_step": {k: v / S for k, v in HOST_MS.items()},
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},

@@ -191,6 +191,7 @@ typedef struct {
   double ms_nn_scan;      /* the k_nearest_wave32 launches alone (part of ms_nearest) */
   uint64_t snap_sum;      /* sum over rounds of the snapshot size T_r */
   uint64_t nn_full_pairs; /* sum over rounds of T_r * B_r: the brute-force scan's pair count */
+  int64_t launches_nn_scan; /* k_nearest_wave32 launches (a one-node first round needs none) */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

@@ -217,6 +217,74 @@ __global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys
   vals[j] = j;
 }
 
+
+// ---- counting sort of n items by a small integer bin: perm lists the items bin by bin.  Used
+// for the longest-first edge order, which only serves load balance -- every result is
+// independent of the order -- so items within a bin keep whatever order the atomics give them.  Three launches and no memset: the scan
+// leaves the histogram zeroed for the next sort (it is zeroed once when allocated).
+constexpr int kCsLdsBins = 1024;  // up to this many bins, per-block LDS histograms
+__global__ __launch_bounds__(256) void k_cs_hist(const int* bin, int n, int nbins, int* hist) {
+  __shared__ int lh[kCsLdsBins];
+  const bool lds = nbins <= kCsLdsBins;
+  if (lds) {
+    for (int b = threadIdx.x; b < nbins; b += 256) lh[b] = 0;
+    __syncthreads();
+  }
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) {
+    if (lds) atomicAdd(&lh[bin[i]], 1);
+    else atomicAdd(&hist[bin[i]], 1);
+  }
+  if (lds) {
+    __syncthreads();
+    for (int b = threadIdx.x; b < nbins; b += 256)
+      if (lh[b]) atomicAdd(&hist[b], lh[b]);
+  }
+}
+// one block: hoff = exclusive scan of hist, hist zeroed
+__global__ __launch_bounds__(1024) void k_cs_scan(int* hist, int nbins, int* hoff) {
+  __shared__ int part[1024];
+  const int t = threadIdx.x;
+  const int per = (nbins + 1023) / 1024, b0 = t * per, b1 = min(nbins, b0 + per);
+  int sum = 0;
+  for (int b = b0; b < b1; ++b) sum += hist[b];
+  part[t] = sum;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {
+    const int x = t >= o ? part[t - o] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int run = part[t] - sum;
+  for (int b = b0; b < b1; ++b) {
+    const int c = hist[b];
+    hoff[b] = run;
+    run += c;
+    hist[b] = 0;
+  }
+}
+// perm[hoff[bin] + rank] = item; with few bins each block reserves its range per bin once
+__global__ __launch_bounds__(256) void k_cs_scatter(const int* bin, int n, int nbins, int* hoff,
+                                                    int* perm) {
+  __shared__ int lc[kCsLdsBins];
+  const bool lds = nbins <= kCsLdsBins;
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int b = i < n ? bin[i] : 0;
+  if (!lds) {
+    if (i < n) perm[atomicAdd(&hoff[b], 1)] = i;
+    return;
+  }
+  for (int k = threadIdx.x; k < nbins; k += 256) lc[k] = 0;
+  __syncthreads();
+  const int r = i < n ? atomicAdd(&lc[b], 1) : 0;
+  __syncthreads();
+  for (int k = threadIdx.x; k < nbins; k += 256)
+    if (lc[k]) lc[k] = atomicAdd(&hoff[k], lc[k]);
+  __syncthreads();
+  if (i < n) perm[lc[b] + r] = i;
+}
+
 #include "tcmp_nn.h"
 #include "tcmp_nn32.h"
 #include "tcmp_insert.h"
@@ -656,10 +724,12 @@ __device__ __forceinline__ bool torque_test_sample(int mode, double mass, const 
 // dynam_fn + final validation + Conf.torques for the planner's path (grid-stride)
 __global__ __launch_bounds__(256) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
                                               double* oq, double* oqd, double* oqdd,
-                                              double* opsg, double* otau) {
+                                              double* opsg, double* otau, long long kcap) {
   const PlanParams P = *Pd;
+  if (st->goal_node < 0) return;
   if (st->status != 0 && st->status != TCMP_PLAN_VALIDATION_FAILED) return;
   const long long K = st->K, ni = st->ni, W = st->W;
+  if (K > kcap) return;  // the host grows the rows and launches again
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < K;
        i += (long long)gridDim.x * blockDim.x) {
     double x[7], v[7], a[7];
@@ -683,9 +753,10 @@ __global__ __launch_bounds__(256) void k_traj(const PlanParams* __restrict__ Pd,
 
 // first_fail uses LLONG_MAX as "none" during the kernel
 __global__ void k_traj_prep(DevState* st) {
-  if (st->status == 0) st->first_fail = LLONG_MAX;
+  if (st->goal_node >= 0 && st->status == 0) st->first_fail = LLONG_MAX;
 }
 __global__ void k_traj_post(DevState* st) {
+  if (st->goal_node < 0) return;
   if (st->first_fail == LLONG_MAX) st->first_fail = -1;
   else if (st->status == 0 && st->first_fail >= 0) st->status = TCMP_PLAN_VALIDATION_FAILED;
 }
@@ -811,6 +882,7 @@ struct RoundGraph {
   std::vector<EventPair> events;
   unsigned long long key = 0;
   int rounds = 0;
+  int scans = 0;
 };
 
 }  // namespace
@@ -875,6 +947,20 @@ struct tcmp_handle {
   int nn_waves_per_cu = 16;
   hipEvent_t ins_ev = nullptr;     // open F_INSERT mark between round_search and round_finish
   DBuf<long long> xch;             // shared-tree round exchange slots (k_sr_*)
+  DBuf<int> cs_hist, cs_hoff;      // counting-sort histogram (kept zeroed) and bin offsets
+  // pinned host staging of a plan's begin / finish (async copies, one host wait per call)
+  struct Pin {
+    double sg[16];     // start, goal rows of 8
+    double root[8];
+    int m1;
+    int2 z;
+    int coll[2];
+    DevState st;
+    PlanParams P;
+  };
+  Pin* pin = nullptr;
+  size_t fin_W = 0, fin_K = 0;  // the finished plan's waypoint / trajectory rows (plan_fetch)
+  long long kcap = 0;           // trajectory rows allocated at plan_begin (exec_time * 1000 + 2)
   int nn_cand_bits = 16;           // top key bits the candidates are sorted by
   DBuf<double> second;
   DBuf<long long> chain;
@@ -893,6 +979,7 @@ struct tcmp_handle {
   bool capturing = false;
   double ms[F_COUNT] = {};
   long long launches_nearest = 0;
+  long long launches_scan = 0;      // k_nearest_wave32 launches of the open plan
   int edge_blocks = 0;
 
   Geo geo() const {
@@ -1012,6 +1099,23 @@ unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>
 // Index buffers for trees of up to N nodes and up to B candidates per scan, plus the sort
 // and scan temporaries they need (shared by the plan's rounds and tcmp_nearest: nothing in
 // them outlives one index build + scan).
+int count_sort(tcmp_handle* h, const int* bin, int n, int nbins, int* perm) {
+  if (n <= 0) return 0;
+  if ((size_t)nbins > h->cs_hist.n) {
+    if (int rc = h->cs_hist.ensure((size_t)nbins)) return rc;
+    if (int rc = h->cs_hoff.ensure((size_t)nbins)) return rc;
+    HIPCHK(hipMemsetAsync(h->cs_hist.p, 0, h->cs_hist.n * sizeof(int), h->stream));
+  }
+  hipLaunchKernelGGL(k_cs_hist, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, bin, n, nbins,
+                     h->cs_hist.p);
+  hipLaunchKernelGGL(k_cs_scan, dim3(1), dim3(1024), 0, h->stream, h->cs_hist.p, nbins,
+                     h->cs_hoff.p);
+  hipLaunchKernelGGL(k_cs_scatter, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, bin, n, nbins,
+                     h->cs_hoff.p, perm);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
 int ensure_index(tcmp_handle* h, size_t N, size_t B) {
   int rc = h->nkeys_in.ensure(N);
   rc = rc ? rc : h->skeys.ensure(N);
@@ -1031,9 +1135,16 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
   rc = rc ? rc : h->ckey.ensure(N);
   rc = rc ? rc : h->chome.ensure(2 * B);
   rc = rc ? rc : h->ckeys_in.ensure(B);
-  rc = rc ? rc : h->ckeys.ensure(B);
   rc = rc ? rc : h->cvals_in.ensure(B);
   rc = rc ? rc : h->cperm.ensure(B);
+  if (rc) return rc;
+  if (h->cs_hist.n < 65536) {  // the counting sorts' histogram, zeroed once (self-cleaning)
+    rc = h->cs_hist.ensure(65536);
+    rc = rc ? rc : h->cs_hoff.ensure(65536);
+    if (rc) return rc;
+    HIPCHK(hipMemsetAsync(h->cs_hist.p, 0, h->cs_hist.n * sizeof(int), h->stream));
+  }
+  rc = h->ckeys.ensure(B);
   if (rc) return rc;
   size_t t1 = 0, t2 = 0, t3 = 0;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(nullptr, t1, h->nkeys_in.p, h->skeys.p, h->nvals_in.p,
@@ -1042,6 +1153,38 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
                                              h->cperm.p, B, 0, 64, h->stream));
   HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, t3, h->cflag.p, h->cid.p, (int)N, h->stream));
   return h->sort_tmp.ensure(std::max(std::max(t1, t2), t3));
+}
+
+// the first round: nearest = the root, score = its exact score (the scan's arithmetic), second
+// bound +inf; also the resets k_nn_home does for the scan and the edge kernel
+__global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const double* cfg,
+                          const double* cand, int nb, int* nn, double* second, double* score) {
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j < 8) st->nn_queue[j] = 0;
+  if (j == 0) {
+    st->nn_counter = 0;
+    st->work_counter = 0;
+  }
+  if (j >= nb) return;
+  const PlanParams P = *Pd;
+  double a[7], s[7];
+  load7(cfg, a);
+  load7(cand + 8 * (size_t)j, s);
+  const double d0 = s[0] - a[0], d1 = s[1] - a[1], d2 = s[2] - a[2], d3 = s[3] - a[3],
+               d4 = s[4] - a[4], d5 = s[5] - a[5], d6 = s[6] - a[6];
+  double dd;
+  if (P.uniform_w) {
+    dd = d0 * d0;
+    dd = fma(d1, d1, dd); dd = fma(d2, d2, dd); dd = fma(d3, d3, dd);
+    dd = fma(d4, d4, dd); dd = fma(d5, d5, dd); dd = fma(d6, d6, dd);
+  } else {
+    dd = P.w[0] * (d0 * d0);
+    dd = fma(P.w[1] * d1, d1, dd); dd = fma(P.w[2] * d2, d2, dd); dd = fma(P.w[3] * d3, d3, dd);
+    dd = fma(P.w[4] * d4, d4, dd); dd = fma(P.w[5] * d5, d5, dd); dd = fma(P.w[6] * d6, d6, dd);
+  }
+  nn[j] = 0;
+  if (second) second[j] = INFINITY;
+  if (score) score[j] = dd;
 }
 
 // Exact nearest node of nb candidates (rows of 8) among the st->n_nodes <= T_bound tree rows
@@ -1053,6 +1196,14 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
                    const double* cfg,
                    long long T_bound, const double* cand, int nb, int* nn, double* second,
                    double* score) {
+  if (T_bound == 1) {
+    // a one-node snapshot (the first round): the root is every candidate's nearest node and
+    // there is no second one -- no index to build
+    hipLaunchKernelGGL(k_nn_root, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, dP, st, cfg,
+                       cand, nb, nn, second, score);
+    HIPCHK(hipGetLastError());
+    return 0;
+  }
   hipLaunchKernelGGL(k_node_keys, dim3(std::min<unsigned>(grid_for(T_bound, 256), 4096)), dim3(256),
                      0, h->stream, st, cfg, T_bound, h->nkeys_in.p, h->nvals_in.p);
   HIPCHK(hipGetLastError());
@@ -1100,15 +1251,14 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, cand, nb,
                      h->ckeys_in.p, h->cvals_in.p);
   HIPCHK(hipGetLastError());
-  // candidates only need locality (the scan order never changes a result): top 16 key bits
-  // for the one-candidate scan, the full key when a wave scans Morton-adjacent groups
+  // candidates only need locality (the scan order never changes a result): their top key
+  // bits (rocPRIM's Onesweep; a 65,536-bin counting sort measured 0.3 ms per query slower)
   tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
                                              h->cvals_in.p, h->cperm.p, (size_t)nb,
-                                             kKeyBits + 1 - h->nn_cand_bits, kKeyBits + 1,
-                                             h->stream));
+                                             kKeyBits - h->nn_cand_bits, kKeyBits, h->stream));
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
-                     h->skeys.p, h->ckeys.p, h->cid.p, h->sid.p, nb, h->chome.p);
+                     h->skeys.p, h->ckeys_in.p, h->cperm.p, h->cid.p, h->sid.p, nb, h->chome.p);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave (k_nn_home
   // cleared the queues)
@@ -1116,6 +1266,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   const int per_wave = (int)((nb + waves - 1) / waves);
   const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
   hipEvent_t e0;
+  h->launches_scan++;
   h->mark_begin(F_NNSCAN, &e0);
 #define TCMP_NNW(UWV, SWV)                                                                   \
   hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(256), 0, h->stream, dP, st, \
@@ -1133,8 +1284,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
 // for longest-first scheduling of k_edges
 constexpr int kEdgeOrderMin = 4096;
 __global__ void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg, const int* nn,
-                                  const double* cand, int nb, unsigned long long* keys,
-                                  int* vals) {
+                                  const double* cand, int nb, int* bins) {
   const PlanParams P = *Pd;
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= nb) return;
@@ -1142,8 +1292,7 @@ __global__ void k_edge_order_keys(const PlanParams* __restrict__ Pd, const doubl
   load7(cfg + 8 * (size_t)nn[e], a);
   load7(cand + 8 * (size_t)e, b);
   const int n = num_steps(a, b, P.res);
-  keys[e] = (unsigned long long)(255 - min(n, 255));
-  vals[e] = e;
+  bins[e] = 255 - min(n, 255);
 }
 
 // reset_counter = false: the plan's k_nn_home already cleared the work counter
@@ -1296,13 +1445,14 @@ int tcmp_create(int device, tcmp_handle** out) {
   }
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
+  HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->pin), sizeof(tcmp_handle::Pin)));
   HIPCHK(hipMalloc(&h->st_nn, sizeof(DevState)));
   HIPCHK(hipMalloc(&h->dP, sizeof(PlanParams)));
   HIPCHK(hipMalloc(&h->dPx, sizeof(PlanParams)));
   HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
-  if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(kKeyBits + 1, std::max(8, atoi(e)));
+  if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(16, std::max(8, atoi(e)));
   *out = h;
   return 0;
 }
@@ -1333,6 +1483,8 @@ int tcmp_destroy(tcmp_handle* h) {
     b->release();
   h->nnscore.release();
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
+  h->cs_hist.release();
+  h->cs_hoff.release();
   for (auto* b : {&h->nvals_in, &h->svals, &h->cvals_in, &h->cperm}) b->release();
   h->stree.release();
   h->stree32.release();
@@ -1364,6 +1516,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->drop_graph();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->st) (void)hipFree(h->st);
+  if (h->pin) (void)hipHostFree(h->pin);
   if (h->st_nn) (void)hipFree(h->st_nn);
   if (h->dP) (void)hipFree(h->dP);
   if (h->dPx) (void)hipFree(h->dPx);
@@ -2004,33 +2157,59 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   h->collect_events();
   for (double& m : h->ms) m = 0;
   h->launches_nearest = 0;
+  h->launches_scan = 0;
+  // the finish's buffers, sized here so that tcmp_plan_finish needs one host wait: waypoints
+  // (bounded by the chain's total n_safe; generous, checked on the device) and trajectory
+  // rows K = (W - 1) * floor(exec_time * 1000 / W) < exec_time * 1000 (k_retrace)
+  {
+    const size_t wcap = std::max<size_t>(1024, N * 64);
+    rc = h->wp.ensure(std::min<size_t>(wcap, (size_t)1 << 26) * 7);
+    const double kc = std::max(0.0, cfg->execution_time) * 1000.0 + 2.0;
+    h->kcap = (long long)std::min(kc, (double)(1 << 22));
+    rc = rc ? rc : h->tq.ensure((size_t)h->kcap * 7);
+    rc = rc ? rc : h->tqd.ensure((size_t)h->kcap * 7);
+    rc = rc ? rc : h->tqdd.ensure((size_t)h->kcap * 7);
+    rc = rc ? rc : h->tpsg.ensure((size_t)h->kcap);
+    rc = rc ? rc : h->ttau.ensure((size_t)h->kcap * 7);
+    rc = rc ? rc : h->s0.ensure(16);
+    rc = rc ? rc : h->i0.ensure(2);
+    if (rc) return rc;
+  }
+  h->fin_W = 0;
+  h->fin_K = 0;
+  // one host wait: every copy is staged in the handle's pinned block
+  tcmp_handle::Pin& pn = *h->pin;
+  memset(pn.sg, 0, sizeof(pn.sg));
+  memcpy(pn.sg, cfg->start, sizeof(double) * 7);
+  memcpy(pn.sg + 8, cfg->goal, sizeof(double) * 7);
   // collision(start) or collision(goal) (rrt_star.py:152)
-  double sg[14];
-  memcpy(sg, cfg->start, sizeof(double) * 7);
-  memcpy(sg + 7, cfg->goal, sizeof(double) * 7);
-  int coll[2] = {0, 0};
-  if ((rc = tcmp_check_configs(h, sg, 2, coll))) return rc;
+  HIPCHK(hipMemcpyAsync(h->s0.p, pn.sg, sizeof(pn.sg), hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
+                     dim3(1), dim3(256), lds_bytes(h), h->stream, h->s0.p, 2LL, h->scene(),
+                     h->geo(), h->i0.p);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pn.coll, h->i0.p, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   // root node (OptimalNode(start), rrt_star.py:155)
-  double root[8] = {0};
-  for (int k = 0; k < 7; ++k) root[k] = cfg->start[k];
-  HIPCHK(hipMemcpyAsync(h->cfg.p, root, sizeof(root), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->tgt.p, root, sizeof(root), hipMemcpyHostToDevice, h->stream));
-  int m1 = -1;
-  HIPCHK(hipMemcpyAsync(h->parent.p, &m1, sizeof(int), hipMemcpyHostToDevice, h->stream));
-  int2 z = make_int2(0, 0);
-  HIPCHK(hipMemcpyAsync(h->meta.p, &z, sizeof(int2), hipMemcpyHostToDevice, h->stream));
-  DevState s;
-  memset(&s, 0, sizeof(s));
-  s.n_nodes = 1;
-  s.goal_node = -1;
-  s.first_fail = -1;
-  s.round_goal = INT_MAX;
-  HIPCHK(hipMemcpyAsync(h->st, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->dP, &h->P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
+  memset(pn.root, 0, sizeof(pn.root));
+  for (int k = 0; k < 7; ++k) pn.root[k] = cfg->start[k];
+  HIPCHK(hipMemcpyAsync(h->cfg.p, pn.root, sizeof(pn.root), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->tgt.p, pn.root, sizeof(pn.root), hipMemcpyHostToDevice, h->stream));
+  pn.m1 = -1;
+  HIPCHK(hipMemcpyAsync(h->parent.p, &pn.m1, sizeof(int), hipMemcpyHostToDevice, h->stream));
+  pn.z = make_int2(0, 0);
+  HIPCHK(hipMemcpyAsync(h->meta.p, &pn.z, sizeof(int2), hipMemcpyHostToDevice, h->stream));
+  memset(&pn.st, 0, sizeof(pn.st));
+  pn.st.n_nodes = 1;
+  pn.st.goal_node = -1;
+  pn.st.first_fail = -1;
+  pn.st.round_goal = INT_MAX;
+  HIPCHK(hipMemcpyAsync(h->st, &pn.st, sizeof(pn.st), hipMemcpyHostToDevice, h->stream));
+  pn.P = h->P;
+  HIPCHK(hipMemcpyAsync(h->dP, &pn.P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->plan_open = true;
   result->n_nodes = 1;
-  result->status = (coll[0] || coll[1]) ? TCMP_PLAN_START_GOAL_COLLISION : TCMP_PLAN_OK;
+  result->status = (pn.coll[0] || pn.coll[1]) ? TCMP_PLAN_START_GOAL_COLLISION : TCMP_PLAN_OK;
   if (result->status) h->plan_open = false;
   return 0;
 }
@@ -2065,7 +2244,8 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
                         (const void*)h->cflag.p, (const void*)h->cid.p, (const void*)h->cstart.p,
                         (const void*)h->sflag.p, (const void*)h->sid.p, (const void*)h->sstart.p,
                         (const void*)h->ckey.p, (const void*)h->chome.p, (const void*)h->ckeys_in.p,
-                        (const void*)h->ckeys.p, (const void*)h->cvals_in.p, (const void*)h->cperm.p,
+                        (const void*)h->cs_hist.p, (const void*)h->cvals_in.p, (const void*)h->cperm.p,
+                        (const void*)h->cs_hoff.p, (const void*)h->ckeys.p,
                         (const void*)h->sort_tmp.p, (const void*)h->bcount.p, (const void*)h->boff.p,
                         (const void*)h->st, (const void*)h->dP})
     mixp(p);
@@ -2143,15 +2323,12 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
   h->mark_begin(F_EDGES, &e0);
   EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p, nullptr};
   if (nb >= kEdgeOrderMin) {
-    // longest planned edges first (the persistent lanes then finish together): 8-bit keys
-    // 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
+    // longest planned edges first (the persistent lanes then finish together): a counting
+    // sort by 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
     hipLaunchKernelGGL(k_edge_order_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP,
-                       h->cfg.p, h->nn.p, h->cand.p, nb, h->ckeys_in.p, h->cvals_in.p);
+                       h->cfg.p, h->nn.p, h->cand.p, nb, h->cvals_in.p);
     HIPCHK(hipGetLastError());
-    size_t tb = h->sort_tmp.n;
-    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
-                                               h->cvals_in.p, h->cperm.p, (size_t)nb, 0, 8,
-                                               h->stream));
+    if (int rc = count_sort(h, h->cvals_in.p, nb, 256, h->cperm.p)) return rc;
     J.order = h->cperm.p;
   }
   if (int rc = launch_edges(h, J, h->dP, false)) return rc;
@@ -2473,7 +2650,8 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
       return run_rounds();
     }
     h->drop_graph();
-    const long long issued = h->samples_issued, launches = h->launches_nearest;
+    const long long issued = h->samples_issued, launches = h->launches_nearest,
+                    scans = h->launches_scan;
     const int last_nb = h->last_nb;
     int rc = 0;
     if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
@@ -2489,6 +2667,7 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
         h->rg.graph = g;
         h->rg.key = key;
         h->rg.rounds = (int)(h->launches_nearest - launches);
+        h->rg.scans = (int)(h->launches_scan - scans);
       } else {
         if (g) (void)hipGraphDestroy(g);
         h->drop_graph();
@@ -2498,6 +2677,7 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
     (void)hipGetLastError();
     h->samples_issued = issued;  // nothing ran yet
     h->launches_nearest = launches;
+    h->launches_scan = scans;
     h->last_nb = last_nb;
     if (rc) {  // capture unsupported here: launch directly from now on
       h->use_graphs = false;
@@ -2507,6 +2687,7 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
   HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
   h->samples_issued += n_samples;
   h->launches_nearest += h->rg.rounds;
+  h->launches_scan += h->rg.scans;
   h->last_nb = (int)(n_samples % batch ? n_samples % batch : batch);
   for (const auto& p : h->rg.events) h->ev_used.push_back(p);
   return 0;
@@ -2516,51 +2697,57 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   if (int rc = set_dev(h)) return rc;
   if (!r) return fail(-1, "null result");
   if (!h->plan_open) return fail(-1, "no open plan");
-  DevState s;
+  memset(r, 0, sizeof(*r));
+  r->first_fail = -1;
+  // retrace + min-jerk + validation are launched unconditionally (they do nothing without a
+  // goal node) into the buffers tcmp_plan_begin sized, so the host waits once
+  hipEvent_t e0;
+  h->mark_begin(F_FINISH, &e0);
+  hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->dP, h->st,
+                     Tree{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p}, h->chain.p, h->wp.p,
+                     (long long)(h->wp.n / 7));
+  auto launch_traj = [&]() {
+    hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
+    hipLaunchKernelGGL(k_traj, dim3(std::min<unsigned>(grid_for(h->kcap, 256), 2048)), dim3(256), 0,
+                       h->stream, h->dP, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
+                       h->ttau.p, h->kcap);
+    hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
+  };
+  launch_traj();
+  HIPCHK(hipGetLastError());
+  h->mark_end(F_FINISH, e0);
+  DevState& s = h->pin->st;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
-  memset(r, 0, sizeof(*r));
   r->goal_node = s.goal_node;
-  r->first_fail = -1;
   if (s.overflow == 1) return fail(-3, "tree capacity exceeded");
+  h->fin_W = 0;
+  h->fin_K = 0;
   if (s.goal_node >= 0) {
-    // capacity for waypoints: bounded by the chain's total n_safe; allocate generously
-    const size_t wcap = std::max<size_t>(1024, (size_t)s.n_nodes * 64);
-    int rc = h->wp.ensure(std::min<size_t>(wcap, (size_t)1 << 26) * 7);
-    if (rc) return rc;
-    hipEvent_t e0;
-    h->mark_begin(F_FINISH, &e0);
-    hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->dP, h->st,
-                       Tree{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p}, h->chain.p, h->wp.p,
-                       (long long)(h->wp.n / 7));
-    HIPCHK(hipGetLastError());
-    long long WK[3];
-    HIPCHK(hipMemcpyAsync(WK, &h->st->W, sizeof(WK), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
-    const long long K = std::max<long long>(WK[2], 1);
-    rc = h->tq.ensure(K * 7);
-    rc = rc ? rc : h->tqd.ensure(K * 7);
-    rc = rc ? rc : h->tqdd.ensure(K * 7);
-    rc = rc ? rc : h->tpsg.ensure(K);
-    rc = rc ? rc : h->ttau.ensure(K * 7);
-    if (rc) return rc;
-    hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
-    hipLaunchKernelGGL(k_traj, dim3(std::min<unsigned>(grid_for(K, 256), 2048)), dim3(256), 0,
-                       h->stream, h->dP, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
-                       h->ttau.p);
-    hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
-    HIPCHK(hipGetLastError());
-    h->mark_end(F_FINISH, e0);
-    HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
     if (s.status == -3) return fail(-3, "waypoint capacity exceeded");
+    if (s.K > h->kcap) {
+      // an execution time past the preallocated rows: grow and run the trajectory again
+      const long long K = s.K;
+      int rc = h->tq.ensure(K * 7);
+      rc = rc ? rc : h->tqd.ensure(K * 7);
+      rc = rc ? rc : h->tqdd.ensure(K * 7);
+      rc = rc ? rc : h->tpsg.ensure(K);
+      rc = rc ? rc : h->ttau.ensure(K * 7);
+      if (rc) return rc;
+      h->kcap = K;
+      launch_traj();
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
+      HIPCHK(hipStreamSynchronize(h->stream));
+    }
     r->n_waypoints = s.W;
     r->n_traj = s.status == TCMP_PLAN_MINJERK_ASSERT ? 0 : s.K;
     r->first_fail = s.first_fail;
     r->status = s.status;
     r->goal_found = 1;
+    h->fin_W = (size_t)s.W;
+    h->fin_K = (size_t)r->n_traj;
   } else {
-    HIPCHK(hipStreamSynchronize(h->stream));
     r->status = TCMP_PLAN_NO_GOAL;
   }
   h->collect_events();
@@ -2577,6 +2764,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   r->ms_rewire = h->ms[F_REWIRE];
   r->ms_finish = h->ms[F_FINISH];
   r->launches_nearest = h->launches_nearest;
+  r->launches_nn_scan = h->launches_scan;
   r->nn_box_tests = s.nn_box_tests;
   r->ms_nn_scan = h->ms[F_NNSCAN];
   r->snap_sum = s.snap_sum;
@@ -2587,11 +2775,9 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
 int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
                     double* psg, double* tau) {
   if (int rc = set_dev(h)) return rc;
-  DevState s;
-  HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
-  if (s.goal_node < 0) return fail(-1, "no plan to fetch");
-  const long long W = s.W, K = s.status == TCMP_PLAN_MINJERK_ASSERT ? 0 : s.K;
+  // the sizes tcmp_plan_finish read (it waited for the plan); no other state read here
+  if (h->fin_W == 0) return fail(-1, "no plan to fetch");
+  const long long W = (long long)h->fin_W, K = (long long)h->fin_K;
   if (waypoints && W)
     HIPCHK(hipMemcpyAsync(waypoints, h->wp.p, W * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   if (K) {

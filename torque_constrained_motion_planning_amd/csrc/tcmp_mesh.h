@@ -75,13 +75,16 @@ __device__ __forceinline__ float facet_pass32(const HullA32& A, const HullB32& B
     }
     mn[j] = INFINITY;
   }
+  // the vertex streams are wave-uniform loads: unrolled so that four are in flight per wait
   if (BF) {
+#pragma unroll 4
     for (int v = A.v0; v < A.v1; ++v) {
       const float x = A.v3[3 * v], y = A.v3[3 * v + 1], z = A.v3[3 * v + 2];
 #pragma unroll
       for (int j = 0; j < J; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
     }
   } else {
+#pragma unroll 4
     for (int v = B.v0; v < B.v1; ++v) {
       const float4 P4 = B.v[v];
 #pragma unroll
@@ -164,7 +167,7 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
     }
     const float el2 = ex * ex + ey * ey + ez * ez;
-#pragma unroll 2
+#pragma unroll 4
     for (int k = B.e0; k < B.e1; ++k) {
       const float* E = B.er + 16 * k;
       const float cx = E[0], cy = E[1], cz = E[2], dx = E[3], dy = E[4], dz = E[5];

@@ -202,11 +202,12 @@ __global__ __launch_bounds__(256) void k_nn_build_blocks(DevState* st, const flo
   }
 }
 
-// home cell of each Morton-sorted candidate: the cell holding its key's lower bound, and its
-// super-cell: home[j] = cell, home[nb + j] = super-cell
+// home cell of each Morton-ordered candidate (j-th in cperm order, its key ckeys[cperm[j]]):
+// the cell holding its key's lower bound, and its super-cell: home[j] = cell, home[nb + j] =
+// super-cell
 __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
-                          const unsigned long long* ckeys, const int* cid, const int* sid, int nb,
-                          int* home) {
+                          const unsigned long long* ckeys, const int* cperm, const int* cid,
+                          const int* sid, int nb, int* home) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < 8) st->nn_queue[j] = 0;  // the scan's per-XCD queues (next launch)
   if (j == 0) {
@@ -215,7 +216,7 @@ __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
   }
   if (j >= nb) return;
   const long long T = st->n_nodes;
-  const unsigned long long k = ckeys[j];
+  const unsigned long long k = ckeys[cperm[j]];
   long long lo = 0, hi = T;
   while (lo < hi) {
     const long long mid = (lo + hi) >> 1;

@@ -49,13 +49,32 @@ __device__ __forceinline__ float box_lb32(const float* b, const float sh[7], con
   const float4 h1 = *reinterpret_cast<const float4*>(b + 12);
   if (start) *start = __float_as_int(l1.w);
   if (count) *count = __float_as_int(h1.w);
-  const float lo[7] = {l0.x, l0.y, l0.z, l0.w, l1.x, l1.y, l1.z};
-  const float hi[7] = {h0.x, h0.y, h0.z, h0.w, h1.x, h1.y, h1.z};
-  float lb = 0.f;
-#pragma unroll
-  for (int k = 0; k < 7; ++k) {
-    const float g = fmaxf(fmaxf(lo[k] - sh[k], sl[k] - hi[k]), 0.f);
-    lb = fmaf(UW ? g : w[k] * g, g, lb);
+  // the two gaps of a coordinate pair per packed subtraction (v_pk_add_f32), the squares
+  // accumulated per pair (v_pk_fma_f32); any association of the seven terms is covered by
+  // the 1e-6 relative scale-down
+  const f32x2 a01 = f32x2{l0.x, l0.y} - f32x2{sh[0], sh[1]};
+  const f32x2 a23 = f32x2{l0.z, l0.w} - f32x2{sh[2], sh[3]};
+  const f32x2 a45 = f32x2{l1.x, l1.y} - f32x2{sh[4], sh[5]};
+  const f32x2 b01 = f32x2{sl[0], sl[1]} - f32x2{h0.x, h0.y};
+  const f32x2 b23 = f32x2{sl[2], sl[3]} - f32x2{h0.z, h0.w};
+  const f32x2 b45 = f32x2{sl[4], sl[5]} - f32x2{h1.x, h1.y};
+  const float a6 = l1.z - sh[6], b6 = sl[6] - h1.z;
+  const f32x2 g01 = {fmaxf(fmaxf(a01.x, b01.x), 0.f), fmaxf(fmaxf(a01.y, b01.y), 0.f)};
+  const f32x2 g23 = {fmaxf(fmaxf(a23.x, b23.x), 0.f), fmaxf(fmaxf(a23.y, b23.y), 0.f)};
+  const f32x2 g45 = {fmaxf(fmaxf(a45.x, b45.x), 0.f), fmaxf(fmaxf(a45.y, b45.y), 0.f)};
+  const float g6 = fmaxf(fmaxf(a6, b6), 0.f);
+  f32x2 acc;
+  float lb;
+  if (UW) {
+    acc = g01 * g01;
+    acc = __builtin_elementwise_fma(g23, g23, acc);
+    acc = __builtin_elementwise_fma(g45, g45, acc);
+    lb = fmaf(g6, g6, acc.x + acc.y);
+  } else {
+    acc = (f32x2{w[0], w[1]} * g01) * g01;
+    acc = __builtin_elementwise_fma(f32x2{w[2], w[3]} * g23, g23, acc);
+    acc = __builtin_elementwise_fma(f32x2{w[4], w[5]} * g45, g45, acc);
+    lb = fmaf(w[6] * g6, g6, acc.x + acc.y);
   }
   return lb * 0.999999f;
 }
