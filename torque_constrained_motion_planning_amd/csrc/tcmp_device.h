@@ -1199,10 +1199,13 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       while (pend) {
         const int L = __builtin_ctzll(pend);
         pend &= pend - 1;
-        const int sL = __shfl(src, L);
+        // wave-uniform by construction; readfirstlane tells the compiler, so the hull data
+        // indexed by them is scalar-loaded
+        const int sL = __builtin_amdgcn_readfirstlane(__shfl(src, L));
         __builtin_amdgcn_wave_barrier();
         if ((*cmask >> sL) & 1ull) continue;  // that lane already collides
-        const int lL = __shfl(lk, L), oL = __shfl(orow, L);
+        const int lL = __builtin_amdgcn_readfirstlane(__shfl(lk, L)),
+                  oL = __builtin_amdgcn_readfirstlane(__shfl(orow, L));
         Pose PL;
 #pragma unroll
         for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);

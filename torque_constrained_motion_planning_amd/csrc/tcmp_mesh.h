@@ -47,6 +47,11 @@ struct HullB32 {
   int v0, v1, f0, f1, e0, e1;
 };
 
+// Wave-uniform streams of read-only hull data go through the constant address space, so they
+// become scalar loads (s_load_dwordx4 / _dwordx16 into SGPRs, the scalar cache) instead of
+// vector loads of one address by every lane.
+typedef const __attribute__((address_space(4))) float cfloat;
+
 // Facet passes: lanes own 64*J facets, the other hull's vertices stream wave-uniformly;
 // returns this lane's minimum of (facet offset - support), INFINITY for empty slots.
 // BF: B's facets (moved into A's frame) against A's vertices; else A's facets (moved into
@@ -77,16 +82,18 @@ __device__ __forceinline__ float facet_pass32(const HullA32& A, const HullB32& B
   }
   // the vertex streams are wave-uniform loads: unrolled so that four are in flight per wait
   if (BF) {
+    cfloat* v3 = (cfloat*)A.v3;
 #pragma unroll 4
     for (int v = A.v0; v < A.v1; ++v) {
-      const float x = A.v3[3 * v], y = A.v3[3 * v + 1], z = A.v3[3 * v + 2];
+      const float x = v3[3 * v], y = v3[3 * v + 1], z = v3[3 * v + 2];
 #pragma unroll
       for (int j = 0; j < J; ++j) mn[j] = fminf(mn[j], nx[j] * x + ny[j] * y + nz[j] * z);
     }
   } else {
+    cfloat* bv = (cfloat*)B.v;
 #pragma unroll 4
     for (int v = B.v0; v < B.v1; ++v) {
-      const float4 P4 = B.v[v];
+      const float4 P4 = make_float4(bv[4 * v], bv[4 * v + 1], bv[4 * v + 2], 0.f);
 #pragma unroll
       for (int j = 0; j < J; ++j) mn[j] = fminf(mn[j], nx[j] * P4.x + ny[j] * P4.y + nz[j] * P4.z);
     }
@@ -167,9 +174,10 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
     }
     const float el2 = ex * ex + ey * ey + ez * ez;
+    cfloat* ber = (cfloat*)B.er;
 #pragma unroll 4
     for (int k = B.e0; k < B.e1; ++k) {
-      const float* E = B.er + 16 * k;
+      cfloat* E = ber + 16 * k;
       const float cx = E[0], cy = E[1], cz = E[2], dx = E[3], dy = E[4], dz = E[5];
       const float cba = cx * ux + cy * uy + cz * uz;
       const float dba = dx * ux + dy * uy + dz * uz;
