@@ -173,8 +173,15 @@ __global__ void k_goal_fix(const PlanParams* __restrict__ Pd, DevState* st, doub
 constexpr int kKeyBits = TCMP_KEY_BITS;
 // rocprim picks a block-sort + merge-sort chain (~15 launches) below 1M items by default;
 // the Onesweep radix sort (one histogram pass + one launch per 8-bit digit) is faster here
+#ifdef TCMP_SORT_BS
+using OnesweepCfg = rocprim::radix_sort_onesweep_config<
+    rocprim::kernel_config<256, 12>, rocprim::kernel_config<TCMP_SORT_BS, TCMP_SORT_IPT>,
+    TCMP_SORT_RB, rocprim::block_radix_rank_algorithm::match>;
+#else
+using OnesweepCfg = rocprim::default_config;
+#endif
 using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                           rocprim::default_config, 16384>;
+                                           OnesweepCfg, 16384>;
 
 __device__ __forceinline__ unsigned long long morton7(const double q[7]) {
   unsigned u[7];
@@ -197,7 +204,9 @@ __global__ void k_node_keys(DevState* st, const double* cfg, long long T_bound,
   const long long T = st->n_nodes;
   for (long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x; n < T_bound;
        n += (long long)gridDim.x * blockDim.x) {
-    unsigned long long key = (1ull << kKeyBits);  // past every real key: sorts last
+    // the largest key: the stable sort puts these nodes (indices >= T) after every real one,
+    // and nothing reads the sorted keys past T
+    unsigned long long key = (1ull << kKeyBits) - 1;
     if (n < T) {
       double q[7];
       load7(cfg + 8 * n, q);
@@ -865,10 +874,11 @@ struct DBuf {
 // F_NNSCAN times the k_nearest_wave launch alone (inside F_NEAREST, not added to totals)
 enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_NNSCAN, F_COUNT };
 
+// one family's span between two recorded events; adjacent families share the boundary event
+// (one record per boundary: each record is an event node of ~5 us in a round graph)
 struct EventPair {
   hipEvent_t a, b;
   int fam;
-  bool owned = false;  // recorded by a cached round graph's event nodes (not pool events)
 };
 
 // A captured sequence of device-sampled rounds (tcmp_plan_run) -- replayed with one
@@ -880,6 +890,7 @@ struct RoundGraph {
   hipGraph_t graph = nullptr;
   hipGraphExec_t exec = nullptr;
   std::vector<EventPair> events;
+  std::vector<hipEvent_t> owned;  // the events its nodes record (destroyed with the graph)
   unsigned long long key = 0;
   int rounds = 0;
   int scans = 0;
@@ -971,7 +982,8 @@ struct tcmp_handle {
   DBuf<int> i0, i1, i2;
   DBuf<unsigned long long> u0;
   // timing
-  std::vector<EventPair> ev_used;
+  std::vector<EventPair> ev_used;   // spans to read at the next collect_events
+  std::vector<hipEvent_t> ev_rec;   // pool events recorded since (returned to the pool there)
   std::vector<hipEvent_t> ev_pool;
   RoundGraph rg;
   unsigned long long rg_seen = 0;  // key seen once: captured when it repeats
@@ -1031,16 +1043,24 @@ struct tcmp_handle {
     if (capturing) (void)hipEventRecordWithFlags(e, stream, hipEventRecordExternal);
     else (void)hipEventRecord(e, stream);
   }
+  hipEvent_t mark() {
+    hipEvent_t e = capturing ? new_event() : get_event();
+    record(e);
+    (capturing ? rg.owned : ev_rec).push_back(e);
+    return e;
+  }
+  void span(int fam, hipEvent_t a, hipEvent_t b) {
+    (capturing ? rg.events : ev_used).push_back(EventPair{a, b, fam});
+  }
   void mark_begin(int fam, hipEvent_t* out) {
-    *out = capturing ? new_event() : get_event();
-    record(*out);
+    *out = mark();
     (void)fam;
   }
-  void mark_end(int fam, hipEvent_t a) {
-    hipEvent_t b = capturing ? new_event() : get_event();
-    record(b);
-    if (capturing) rg.events.push_back(EventPair{a, b, fam, true});
-    else ev_used.push_back(EventPair{a, b, fam, false});
+  // ends family fam at a new event and returns it (the next family's begin, if adjacent)
+  hipEvent_t mark_end(int fam, hipEvent_t a) {
+    const hipEvent_t b = mark();
+    span(fam, a, b);
+    return b;
   }
   hipEvent_t new_event() {
     hipEvent_t e;
@@ -1051,20 +1071,15 @@ struct tcmp_handle {
     for (auto& p : ev_used) {
       float t = 0;
       if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) ms[p.fam] += t;
-      if (!p.owned) {
-        ev_pool.push_back(p.a);
-        ev_pool.push_back(p.b);
-      }
     }
     ev_used.clear();
+    for (auto e : ev_rec) ev_pool.push_back(e);
+    ev_rec.clear();
   }
   void drop_graph() {
     if (rg.exec) (void)hipGraphExecDestroy(rg.exec);
     if (rg.graph) (void)hipGraphDestroy(rg.graph);
-    for (auto& p : rg.events) {
-      (void)hipEventDestroy(p.a);
-      (void)hipEventDestroy(p.b);
-    }
+    for (auto e : rg.owned) (void)hipEventDestroy(e);
     rg = RoundGraph{};
   }
 };
@@ -1195,7 +1210,7 @@ __global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const
 int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, DevState* st,
                    const double* cfg,
                    long long T_bound, const double* cand, int nb, int* nn, double* second,
-                   double* score) {
+                   double* score, hipEvent_t* scan_end = nullptr) {
   if (T_bound == 1) {
     // a one-node snapshot (the first round): the root is every candidate's nearest node and
     // there is no second one -- no index to build
@@ -1210,7 +1225,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   size_t tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
                                              h->nvals_in.p, h->svals.p, (size_t)T_bound, 0,
-                                             kKeyBits + 1, h->stream));
+                                             kKeyBits, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, st,
                      cfg, h->svals.p, h->stree.p, h->stree32.p, T_bound, h->cflag.p, h->sflag.p);
@@ -1264,19 +1279,20 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   // cleared the queues)
   const long long waves = std::min<long long>(nb, (long long)h->cu_count * h->nn_waves_per_cu);
   const int per_wave = (int)((nb + waves - 1) / waves);
-  const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, 256);
+  const unsigned blocks = grid_for((nb + per_wave - 1) / per_wave * 64, kNnBlock);
   hipEvent_t e0;
   h->launches_scan++;
   h->mark_begin(F_NNSCAN, &e0);
 #define TCMP_NNW(UWV, SWV)                                                                   \
-  hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(256), 0, h->stream, dP, st, \
+  hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(kNnBlock), 0, h->stream, dP, st, \
                      h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,          \
                      h->cperm.p, h->chome.p, nb, nn, second, score)
   // four cells per scan round (eight measured slower: 137 VGPRs cost a wave per SIMD)
   if (P.uniform_w) TCMP_NNW(true, 4); else TCMP_NNW(false, 4);
 #undef TCMP_NNW
   HIPCHK(hipGetLastError());
-  h->mark_end(F_NNSCAN, e0);
+  const hipEvent_t e1 = h->mark_end(F_NNSCAN, e0);
+  if (scan_end) *scan_end = e1;
   return 0;
 }
 
@@ -1508,11 +1524,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->second.release();
   h->chain.release();
   h->u0.release();
-  for (auto& p : h->ev_used) {
-    if (p.owned) continue;
-    (void)hipEventDestroy(p.a);
-    (void)hipEventDestroy(p.b);
-  }
+  for (auto e : h->ev_rec) (void)hipEventDestroy(e);
   h->drop_graph();
   for (auto e : h->ev_pool) (void)hipEventDestroy(e);
   if (h->st) (void)hipFree(h->st);
@@ -2034,7 +2046,7 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
   memset(&s, 0, sizeof(s));
   s.n_nodes = T;
   HIPCHK(hipMemcpyAsync(h->st_nn, &s, sizeof(s), hipMemcpyHostToDevice, h->stream));
-  const size_t ev_before = h->ev_used.size();
+  const size_t ev_before = h->ev_used.size(), rec_before = h->ev_rec.size();
   HIPCHK(hipMemcpyAsync(h->dPx, &P, sizeof(P), hipMemcpyHostToDevice, h->stream));
   rc = launch_nearest(h, P, h->dPx, h->st_nn, h->s0.p, T, h->s1.p, (int)n, h->i0.p, h->s2.p,
                       nullptr);
@@ -2042,10 +2054,10 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
   HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   // the scan's timing events belong to no plan
-  while (h->ev_used.size() > ev_before) {
-    h->ev_pool.push_back(h->ev_used.back().a);
-    h->ev_pool.push_back(h->ev_used.back().b);
-    h->ev_used.pop_back();
+  h->ev_used.resize(ev_before);
+  while (h->ev_rec.size() > rec_before) {
+    h->ev_pool.push_back(h->ev_rec.back());
+    h->ev_rec.pop_back();
   }
   return 0;
 }
@@ -2311,16 +2323,17 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
     HIPCHK(hipGetLastError());
   }
   // the snapshot holds at most 1 + (samples issued before this round) nodes
+  hipEvent_t e1 = nullptr;  // the scan's end event also ends the family and begins the edges
   {
     const long long T_bound = 1 + h->samples_issued - B;
     if (int rc = launch_nearest(h, P, h->dP, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
-                                h->second.p, h->nnscore.p))
+                                h->second.p, h->nnscore.p, &e1))
       return rc;
   }
   h->last_nb = nb;
-  h->mark_end(F_NEAREST, e0);
+  if (!e1) e1 = h->mark();
+  h->span(F_NEAREST, e0, e1);
   h->launches_nearest++;
-  h->mark_begin(F_EDGES, &e0);
   EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p, nullptr};
   if (nb >= kEdgeOrderMin) {
     // longest planned edges first (the persistent lanes then finish together): a counting
@@ -2332,8 +2345,7 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
     J.order = h->cperm.p;
   }
   if (int rc = launch_edges(h, J, h->dP, false)) return rc;
-  h->mark_end(F_EDGES, e0);
-  h->mark_begin(F_INSERT, &h->ins_ev);
+  h->ins_ev = h->mark_end(F_EDGES, e1);
   {
     const int nblk = (int)grid_for(nb, 256);
     if (int rc = h->bcount.ensure(nblk)) return rc;
@@ -2363,9 +2375,7 @@ static int round_finish(tcmp_handle* h, int32_t nb) {
   Tree tr{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p};
   hipLaunchKernelGGL(k_ins_final, dim3(1), dim3(1), 0, h->stream, h->dP, h->st, nb);
   HIPCHK(hipGetLastError());
-  h->mark_end(F_INSERT, h->ins_ev);
-  hipEvent_t e0;
-  h->mark_begin(F_REWIRE, &e0);
+  const hipEvent_t e0 = h->mark_end(F_INSERT, h->ins_ev);
   hipLaunchKernelGGL(k_rewire_scan, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
                      tr, h->rwlist.p, h->nbr.p, h->ncount.p);
   HIPCHK(hipGetLastError());

@@ -80,13 +80,23 @@ __device__ __forceinline__ float box_lb32(const float* b, const float sh[7], con
 }
 
 #ifndef TCMP_NN_MINB
-#define TCMP_NN_MINB 1  // min 256-thread blocks per CU the register allocation must allow
+#define TCMP_NN_MINB 1  // min blocks per CU the register allocation must allow
 #endif
+// The scan's workgroups are 1024 threads (16 waves, one workgroup per CU at 4 waves per SIMD)
+// and hold the super-cell boxes in LDS when there are at most kNnLdsSup of them (64 KB): the
+// super-cell tests then cost an LDS round trip instead of an L2 one, and the block level (whose
+// only job is to save super-cell box loads) is skipped.  Larger indexes walk the blocks from
+// global memory as before.  (One walk over a flat pointer serving both was 5 % slower.)
+constexpr int kNnBlock = 1024;
+#ifndef TCMP_NN_LDS_SUP
+#define TCMP_NN_LDS_SUP 1024
+#endif
+constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
 // SW: cells per scan round (4 or 8).  Passing cells queue up across super-cells (the queue
 // holds at most SW) and a round loads all their rows at once: fewer dependent round trips
 // per candidate than one round per super-cell.
 template <bool UW, int SW>
-__global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
+__global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
                                                         const float* sbox, const float* bbox,
@@ -96,7 +106,15 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
   const PlanParams P = *Pd;
   const int lane = lane_id();
   const long long T = st->n_nodes;
-  const int nch = st->nn_cells, nsup = st->nn_supers;
+  const int nsup = st->nn_supers;
+  __shared__ float4 lsup[4 * kNnLdsSup];
+  const bool sup_lds = nsup <= kNnLdsSup;
+  if (sup_lds) {
+    const float4* g4 = reinterpret_cast<const float4*>(sbox);
+    for (int i = threadIdx.x; i < 4 * nsup; i += blockDim.x) lsup[i] = g4[i];
+    __syncthreads();
+  }
+  const float* lsupf = reinterpret_cast<const float*>(lsup);
   double w[7], wsum = 0;
   float w32[7];
 #pragma unroll
@@ -312,25 +330,38 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
       imp = false;
     }
     NN_TICK(0);
-    // blocks of 64 super-cells, zig-zagging out from the home block (one box test each);
-    // a passing block's super-cells are tested one per lane, starting at the home super
-    const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
-    for (int gb = 0; gb < nblk; gb += 64) {
-      const int bidx = zigzag(hb, gb + lane, nblk);
-      const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, sh, sl32, w32) : INFINITY;
-      tests += (unsigned long long)min(64, nblk - gb);
-      uint64_t bmask = __ballot(lbb <= thr);
-      while (bmask) {
-        const int ib = __builtin_ctzll(bmask);
-        bmask &= bmask - 1;
-        if (readlane_f(lbb, ib) > thr) continue;
-        const int blk = __builtin_amdgcn_readlane(bidx, ib);
-        const int rot = blk == hb ? (hs & 63) : 0;
-        const int sidx = 64 * blk + ((lane + rot) & 63);
+    // the cells of a passing super-cell: one box test per lane, passing cells to the queue
+    auto super_cells = [&](int S0, int Sn) {
+      const int c = S0 + lane;
+      const bool cv = lane < Sn && c != hc;
+      int cst = 0, ccn = 0;
+      const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, sh, sl32, w32, &cst, &ccn) : INFINITY;
+      tests += (unsigned long long)Sn;
+#ifdef TCMP_PROF
+      ++pv[1];
+#endif
+      uint64_t cmask = __ballot(lbc <= thr);
+      NN_TICK(2);
+      while (cmask) {
+        const int k = __builtin_ctzll(cmask);
+        cmask &= cmask - 1;
+        if (readlane_f(lbc, k) <= thr) {
+#ifdef TCMP_PROF
+          ++pv[2];
+#endif
+          push(__builtin_amdgcn_readlane(cst, k), __builtin_amdgcn_readlane(ccn, k));
+        }
+      }
+      NN_TICK(3);
+    };
+    if (sup_lds) {
+      // super-cells from LDS, 64 per test round, zig-zagging out from the home super-cell
+      for (int gs = 0; gs < nsup; gs += 64) {
+        const int sidx = zigzag(hs, gs + lane, nsup);
         int sc0 = 0, scn = 0;
         const float lbs =
-            sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
-        tests += (unsigned long long)min(64, nsup - 64 * blk);
+            sidx >= 0 ? box_lb32<UW>(lsupf + 16 * sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
+        tests += (unsigned long long)min(64, nsup - gs);
 #ifdef TCMP_PROF
         ++pv[0];
 #endif
@@ -340,28 +371,40 @@ __global__ __launch_bounds__(256, TCMP_NN_MINB) void k_nearest_wave32(const Plan
           const int i = __builtin_ctzll(smask);
           smask &= smask - 1;
           if (readlane_f(lbs, i) > thr) continue;
-          const int S0 = __builtin_amdgcn_readlane(sc0, i), Sn = __builtin_amdgcn_readlane(scn, i);
-          const int c = S0 + lane;
-          const bool cv = lane < Sn && c != hc;
-          int cst = 0, ccn = 0;
-          const float lbc = cv ? box_lb32<UW>(cbox + 16 * (size_t)c, sh, sl32, w32, &cst, &ccn) : INFINITY;
-          tests += (unsigned long long)Sn;
+          super_cells(__builtin_amdgcn_readlane(sc0, i), __builtin_amdgcn_readlane(scn, i));
+        }
+      }
+    } else {
+      // blocks of 64 super-cells, zig-zagging out from the home block (one box test each);
+      // a passing block's super-cells are tested one per lane, starting at the home super
+      const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
+      for (int gb = 0; gb < nblk; gb += 64) {
+        const int bidx = zigzag(hb, gb + lane, nblk);
+        const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, sh, sl32, w32) : INFINITY;
+        tests += (unsigned long long)min(64, nblk - gb);
+        uint64_t bmask = __ballot(lbb <= thr);
+        while (bmask) {
+          const int ib = __builtin_ctzll(bmask);
+          bmask &= bmask - 1;
+          if (readlane_f(lbb, ib) > thr) continue;
+          const int blk = __builtin_amdgcn_readlane(bidx, ib);
+          const int rot = blk == hb ? (hs & 63) : 0;
+          const int sidx = 64 * blk + ((lane + rot) & 63);
+          int sc0 = 0, scn = 0;
+          const float lbs =
+              sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
+          tests += (unsigned long long)min(64, nsup - 64 * blk);
 #ifdef TCMP_PROF
-          ++pv[1];
+          ++pv[0];
 #endif
-          uint64_t cmask = __ballot(lbc <= thr);
-          NN_TICK(2);
-          while (cmask) {
-            const int k = __builtin_ctzll(cmask);
-            cmask &= cmask - 1;
-            if (readlane_f(lbc, k) <= thr) {
-#ifdef TCMP_PROF
-              ++pv[2];
-#endif
-              push(__builtin_amdgcn_readlane(cst, k), __builtin_amdgcn_readlane(ccn, k));
-            }
+          uint64_t smask = __ballot(lbs <= thr);
+          NN_TICK(1);
+          while (smask) {
+            const int i = __builtin_ctzll(smask);
+            smask &= smask - 1;
+            if (readlane_f(lbs, i) > thr) continue;
+            super_cells(__builtin_amdgcn_readlane(sc0, i), __builtin_amdgcn_readlane(scn, i));
           }
-          NN_TICK(3);
         }
       }
     }
