@@ -151,13 +151,19 @@ __global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long l
 // ------------------------------------------------------------------------------------------
 // k_goal_fix: the round's goal-biased lane takes the goal configuration (rrt_star.py:160-161)
 // ------------------------------------------------------------------------------------------
-__global__ void k_goal_fix(const PlanParams* __restrict__ Pd, DevState* st, double* cand, unsigned char* cgoal, int nb) {
-  const PlanParams P = *Pd;
+// Done by the first kernel of the round's nearest search (k_node_keys or k_nn_root), which
+// runs after k_sample has chosen the lane and before anything reads the candidates.
+struct GoalFix {
+  double* cand;          // null: no fix (host-supplied samples, tcmp_nearest)
+  unsigned char* cgoal;
+};
+__device__ __forceinline__ void goal_fix(const PlanParams* __restrict__ Pd, DevState* st,
+                                         GoalFix gf, int nb) {
   const int j = st->round_goal;
-  if (threadIdx.x == 0 && j < nb) {
+  if (gf.cand && j < nb) {
 #pragma unroll
-    for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = P.goal[k];
-    cgoal[j] = 1;
+    for (int k = 0; k < 7; ++k) gf.cand[8 * (size_t)j + k] = Pd->goal[k];
+    gf.cgoal[j] = 1;
   }
 }
 
@@ -200,7 +206,9 @@ __device__ __forceinline__ unsigned long long morton7(const double q[7]) {
 }
 
 __global__ void k_node_keys(DevState* st, const double* cfg, long long T_bound,
-                            unsigned long long* keys, int* vals) {
+                            unsigned long long* keys, int* vals, const PlanParams* __restrict__ Pd,
+                            GoalFix gf, int nb) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) goal_fix(Pd, st, gf, nb);
   const long long T = st->n_nodes;
   for (long long n = (long long)blockIdx.x * blockDim.x + threadIdx.x; n < T_bound;
        n += (long long)gridDim.x * blockDim.x) {
@@ -217,13 +225,23 @@ __global__ void k_node_keys(DevState* st, const double* cfg, long long T_bound,
   }
 }
 
-__global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys, int* vals) {
+// vals: the candidate's index for the radix sort, or (cbits > 0) its top-cbits key bin for the
+// counting sort
+__global__ void k_cand_keys(const double* cand, int nb, unsigned long long* keys, int* vals,
+                            int cbits, int* hist) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
   double q[7];
   load7(cand + 8 * (size_t)j, q);
-  keys[j] = morton7(q) >> (63 - kKeyBits);
-  vals[j] = j;
+  const unsigned long long k = morton7(q) >> (63 - kKeyBits);
+  keys[j] = k;
+  if (cbits > 0) {
+    const int b = (int)(k >> (kKeyBits - cbits));
+    vals[j] = b;
+    atomicAdd(&hist[b], 1);  // the counting sort's histogram
+  } else {
+    vals[j] = j;
+  }
 }
 
 
@@ -314,6 +332,7 @@ struct EdgeJob {
   int* nsteps;
   double* last;             // stride 8
   const int* order;         // nullable: the k-th edge taken is order[k] (longest first)
+  int* accepted;            // nullable: accepted edges (nsafe > 0) per 256 edges, cleared before
 };
 
 #ifndef TCMP_EDGE_MINW
@@ -420,6 +439,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
         ++i;
       }
       if (!ok || i == n) {
+        if (J.accepted && i > 0) atomicAdd(&J.accepted[e >> 8], 1);
         J.nsafe[e] = i;
         J.nsteps[e] = n;
         store7(J.last + 8 * (size_t)e, q);
@@ -973,6 +993,7 @@ struct tcmp_handle {
   size_t fin_W = 0, fin_K = 0;  // the finished plan's waypoint / trajectory rows (plan_fetch)
   long long kcap = 0;           // trajectory rows allocated at plan_begin (exec_time * 1000 + 2)
   int nn_cand_bits = 16;           // top key bits the candidates are sorted by
+  int nn_cand_count_bits = 12;     // > 0: a counting sort by that many top bits instead (0: the radix sort)
   DBuf<double> second;
   DBuf<long long> chain;
   DBuf<double> wp, tq, tqd, tqdd, tpsg, ttau;
@@ -1114,15 +1135,18 @@ unsigned grid_for(long long n, int block) { return (unsigned)std::max<long long>
 // Index buffers for trees of up to N nodes and up to B candidates per scan, plus the sort
 // and scan temporaries they need (shared by the plan's rounds and tcmp_nearest: nothing in
 // them outlives one index build + scan).
-int count_sort(tcmp_handle* h, const int* bin, int n, int nbins, int* perm) {
+// hist_done: the bins' producer already added them to h->cs_hist (ensure_index sized it)
+int count_sort(tcmp_handle* h, const int* bin, int n, int nbins, int* perm, bool hist_done = false) {
   if (n <= 0) return 0;
   if ((size_t)nbins > h->cs_hist.n) {
+    if (hist_done) return fail(-1, "counting sort histogram too small");
     if (int rc = h->cs_hist.ensure((size_t)nbins)) return rc;
     if (int rc = h->cs_hoff.ensure((size_t)nbins)) return rc;
     HIPCHK(hipMemsetAsync(h->cs_hist.p, 0, h->cs_hist.n * sizeof(int), h->stream));
   }
-  hipLaunchKernelGGL(k_cs_hist, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, bin, n, nbins,
-                     h->cs_hist.p);
+  if (!hist_done)
+    hipLaunchKernelGGL(k_cs_hist, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, bin, n, nbins,
+                       h->cs_hist.p);
   hipLaunchKernelGGL(k_cs_scan, dim3(1), dim3(1024), 0, h->stream, h->cs_hist.p, nbins,
                      h->cs_hoff.p);
   hipLaunchKernelGGL(k_cs_scatter, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, bin, n, nbins,
@@ -1173,18 +1197,27 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
 // the first round: nearest = the root, score = its exact score (the scan's arithmetic), second
 // bound +inf; also the resets k_nn_home does for the scan and the edge kernel
 __global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const double* cfg,
-                          const double* cand, int nb, int* nn, double* second, double* score) {
+                          const double* cand, int nb, int* nn, double* second, double* score,
+                          GoalFix gf, int* bcount) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < 8) st->nn_queue[j] = 0;
   if (j == 0) {
     st->nn_counter = 0;
     st->work_counter = 0;
   }
+  if (bcount && j < (nb + 255) / 256) bcount[j] = 0;  // k_edges' accepted-edge counts per 256 lanes
   if (j >= nb) return;
   const PlanParams P = *Pd;
   double a[7], s[7];
   load7(cfg, a);
-  load7(cand + 8 * (size_t)j, s);
+  // the goal lane's candidate is the goal (its thread substitutes it: nothing else reads it here)
+  if (gf.cand && j == st->round_goal) {
+    goal_fix(Pd, st, gf, nb);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) s[k] = P.goal[k];
+  } else {
+    load7(cand + 8 * (size_t)j, s);
+  }
   const double d0 = s[0] - a[0], d1 = s[1] - a[1], d2 = s[2] - a[2], d3 = s[3] - a[3],
                d4 = s[4] - a[4], d5 = s[5] - a[5], d6 = s[6] - a[6];
   double dd;
@@ -1210,17 +1243,18 @@ __global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const
 int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, DevState* st,
                    const double* cfg,
                    long long T_bound, const double* cand, int nb, int* nn, double* second,
-                   double* score, hipEvent_t* scan_end = nullptr) {
+                   double* score, hipEvent_t* scan_end = nullptr, GoalFix gf = GoalFix{},
+                   int* bcount = nullptr) {
   if (T_bound == 1) {
     // a one-node snapshot (the first round): the root is every candidate's nearest node and
     // there is no second one -- no index to build
     hipLaunchKernelGGL(k_nn_root, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, dP, st, cfg,
-                       cand, nb, nn, second, score);
+                       cand, nb, nn, second, score, gf, bcount);
     HIPCHK(hipGetLastError());
     return 0;
   }
   hipLaunchKernelGGL(k_node_keys, dim3(std::min<unsigned>(grid_for(T_bound, 256), 4096)), dim3(256),
-                     0, h->stream, st, cfg, T_bound, h->nkeys_in.p, h->nvals_in.p);
+                     0, h->stream, st, cfg, T_bound, h->nkeys_in.p, h->nvals_in.p, dP, gf, nb);
   HIPCHK(hipGetLastError());
   size_t tb = h->sort_tmp.n;
   HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
@@ -1264,16 +1298,22 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
                      h->stream, st, h->sboxf.p, h->bboxf.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_cand_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, cand, nb,
-                     h->ckeys_in.p, h->cvals_in.p);
+                     h->ckeys_in.p, h->cvals_in.p, h->nn_cand_count_bits, h->cs_hist.p);
   HIPCHK(hipGetLastError());
   // candidates only need locality (the scan order never changes a result): their top key
   // bits (rocPRIM's Onesweep; a 65,536-bin counting sort measured 0.3 ms per query slower)
-  tb = h->sort_tmp.n;
-  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
-                                             h->cvals_in.p, h->cperm.p, (size_t)nb,
-                                             kKeyBits - h->nn_cand_bits, kKeyBits, h->stream));
+  if (h->nn_cand_count_bits > 0) {
+    if (int rc = count_sort(h, h->cvals_in.p, nb, 1 << h->nn_cand_count_bits, h->cperm.p, true))
+      return rc;
+  } else {
+    tb = h->sort_tmp.n;
+    HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->ckeys_in.p, h->ckeys.p,
+                                               h->cvals_in.p, h->cperm.p, (size_t)nb,
+                                               kKeyBits - h->nn_cand_bits, kKeyBits, h->stream));
+  }
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
-                     h->skeys.p, h->ckeys_in.p, h->cperm.p, h->cid.p, h->sid.p, nb, h->chome.p);
+                     h->skeys.p, h->ckeys_in.p, h->cperm.p, h->cid.p, h->sid.p, nb, h->chome.p,
+                     bcount);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave (k_nn_home
   // cleared the queues)
@@ -1299,16 +1339,25 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
 // planned step count of each round edge (nearest node -> candidate) as an ascending sort key
 // for longest-first scheduling of k_edges
 constexpr int kEdgeOrderMin = 4096;
-__global__ void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg, const int* nn,
-                                  const double* cand, int nb, int* bins) {
-  const PlanParams P = *Pd;
+// (the counting sort's histogram is built here too: one launch fewer)
+__global__ __launch_bounds__(256) void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg,
+                                                         const int* nn, const double* cand, int nb,
+                                                         int* bins, int* hist) {
+  __shared__ int lh[256];
+  lh[threadIdx.x] = 0;
+  __syncthreads();
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= nb) return;
-  double a[7], b[7];
-  load7(cfg + 8 * (size_t)nn[e], a);
-  load7(cand + 8 * (size_t)e, b);
-  const int n = num_steps(a, b, P.res);
-  bins[e] = 255 - min(n, 255);
+  if (e < nb) {
+    double a[7], b[7];
+    load7(cfg + 8 * (size_t)nn[e], a);
+    load7(cand + 8 * (size_t)e, b);
+    const int n = num_steps(a, b, Pd->res);
+    const int bin = 255 - min(n, 255);
+    bins[e] = bin;
+    atomicAdd(&lh[bin], 1);
+  }
+  __syncthreads();
+  if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
 }
 
 // reset_counter = false: the plan's k_nn_home already cleared the work counter
@@ -1469,6 +1518,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
   if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(16, std::max(8, atoi(e)));
+  if (const char* e = getenv("TCMP_NN_CSORT")) h->nn_cand_count_bits = std::min(16, std::max(0, atoi(e)));
   *out = h;
   return 0;
 }
@@ -2244,6 +2294,7 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
   mix((unsigned long long)lds_bytes(h));
   mix((unsigned long long)h->nn_waves_per_cu);
   mix((unsigned long long)h->nn_cand_bits);
+  mix((unsigned long long)h->nn_cand_count_bits);
   mix((unsigned long long)h->sort_tmp.n);
   for (const void* p : {(const void*)h->cfg.p, (const void*)h->tgt.p, (const void*)h->parent.p,
                         (const void*)h->meta.p, (const void*)h->cand.p, (const void*)h->last.p,
@@ -2317,17 +2368,16 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
   const PlanParams& P = h->P;
   hipEvent_t e0;
   h->mark_begin(F_NEAREST, &e0);
-  if (device_samples) {
-    hipLaunchKernelGGL(k_goal_fix, dim3(1), dim3(64), 0, h->stream, h->dP, h->st, h->cand.p,
-                       h->cgoal.p, nb);
-    HIPCHK(hipGetLastError());
-  }
+  const GoalFix gf{device_samples ? h->cand.p : nullptr, h->cgoal.p};
+  const int nblk = (int)grid_for(nb, 256);
+  if (int rc = h->bcount.ensure(nblk)) return rc;
+  if (int rc = h->boff.ensure(nblk)) return rc;
   // the snapshot holds at most 1 + (samples issued before this round) nodes
   hipEvent_t e1 = nullptr;  // the scan's end event also ends the family and begins the edges
   {
     const long long T_bound = 1 + h->samples_issued - B;
     if (int rc = launch_nearest(h, P, h->dP, h->st, h->cfg.p, T_bound, h->cand.p, nb, h->nn.p,
-                                h->second.p, h->nnscore.p, &e1))
+                                h->second.p, h->nnscore.p, &e1, gf, h->bcount.p))
       return rc;
   }
   h->last_nb = nb;
@@ -2339,23 +2389,19 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
     // longest planned edges first (the persistent lanes then finish together): a counting
     // sort by 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
     hipLaunchKernelGGL(k_edge_order_keys, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP,
-                       h->cfg.p, h->nn.p, h->cand.p, nb, h->cvals_in.p);
+                       h->cfg.p, h->nn.p, h->cand.p, nb, h->cvals_in.p, h->cs_hist.p);
     HIPCHK(hipGetLastError());
-    if (int rc = count_sort(h, h->cvals_in.p, nb, 256, h->cperm.p)) return rc;
+    if (int rc = count_sort(h, h->cvals_in.p, nb, 256, h->cperm.p, true)) return rc;
     J.order = h->cperm.p;
   }
+  // k_edges counts the accepted edges per 256 lanes (bcount, cleared by the nearest search's
+  // first kernel); the scan turns them into the insertion offsets
+  J.accepted = h->bcount.p;
   if (int rc = launch_edges(h, J, h->dP, false)) return rc;
   h->ins_ev = h->mark_end(F_EDGES, e1);
-  {
-    const int nblk = (int)grid_for(nb, 256);
-    if (int rc = h->bcount.ensure(nblk)) return rc;
-    if (int rc = h->boff.ensure(nblk)) return rc;
-    hipLaunchKernelGGL(k_ins_count, dim3(nblk), dim3(256), 0, h->stream, h->nsafe.p, nb,
-                       h->bcount.p);
-    hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
-                       h->boff.p);
-    HIPCHK(hipGetLastError());
-  }
+  hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
+                     h->boff.p);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 

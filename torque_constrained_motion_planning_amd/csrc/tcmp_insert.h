@@ -1,21 +1,12 @@
 // tcmp_insert.h -- lane-ordered insertion of a round's accepted edges (rrt_star.py:173-180),
-// as a device-wide scan: count per 256-lane block, one-block scan of the counts, then every
-// block writes its nodes at (snapshot size + block offset + in-block rank).  Node order is
-// therefore lane order, exactly as the single-pass reference loop appends them.  In a
-// shared-tree round (tcmp_plan_run_shared) the engines own consecutive lane ranges and add
-// ins_off = the lower ranks' accepted edges, so the global order is still lane order.
+// as a device-wide scan: k_edges counts the accepted edges per 256 lanes as they finish, one
+// block scans the counts, then every block writes its nodes at (snapshot size + block offset +
+// in-block rank).  Node order is therefore lane order, exactly as the single-pass reference
+// loop appends them.  In a shared-tree round (tcmp_plan_run_shared) the engines own
+// consecutive lane ranges and add ins_off = the lower ranks' accepted edges, so the global
+// order is still lane order.
 // Included by tcmp_engine.hip after the state types.
 #pragma once
-
-__global__ __launch_bounds__(256) void k_ins_count(const int* nsafe, int nb, int* bcount) {
-  __shared__ int wc[4];
-  const int j = blockIdx.x * 256 + threadIdx.x;
-  const bool v = j < nb && nsafe[j] > 0;
-  const int c = (int)__popcll(__ballot(v));
-  if (lane_id() == 0) wc[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) bcount[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
-}
 
 __global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcount, int nblocks,
                                                    int* boff) {

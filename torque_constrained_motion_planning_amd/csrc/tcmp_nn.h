@@ -207,9 +207,10 @@ __global__ __launch_bounds__(256) void k_nn_build_blocks(DevState* st, const flo
 // super-cell
 __global__ void k_nn_home(DevState* st, const unsigned long long* skeys,
                           const unsigned long long* ckeys, const int* cperm, const int* cid,
-                          const int* sid, int nb, int* home) {
+                          const int* sid, int nb, int* home, int* bcount) {
   const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j < 8) st->nn_queue[j] = 0;  // the scan's per-XCD queues (next launch)
+  if (bcount && j < (nb + 255) / 256) bcount[j] = 0;  // k_edges' accepted-edge counts
   if (j == 0) {
     st->nn_counter = 0;
     st->work_counter = 0;          // k_edges' lane-refill counter (launched after the scan)

@@ -17,6 +17,14 @@
 // k_ins_write's rewire flag (a "may need the neighbour scan" test) stays conservative, and the
 // neighbour scan itself is exact.  Pruning uses the exact fp64 best, as before.
 //
+// The pruning threshold is the nearest search's own, thr >= m (rounded up): every node the scan
+// never looked at is farther than the final thr, so second = min(second over the nodes looked
+// at, thr) is still a lower bound of the true second-smallest distance.  k_ins_write flags a
+// new node for the neighbour scan when second < (|q_new - s| + r)^2; that ball lies inside the
+// searched one unless the edge advanced less than r, and then second <= thr < (.. + r)^2 flags
+// it anyway.  (Round 1 padded the threshold to (sqrt(m) + r)^2 instead, so that `second` was
+// exact out to the rewire ball: a 7-D search ball a few percent wider.)
+//
 // Work distribution: eight queues, one per XCD, each over a contiguous eighth of the
 // Morton-sorted candidates; a wave pulls batches of four from its own XCD's queue
 // (HW_REG_XCC_ID) so the nodes one XCD touches stay in its L2, and moves on to the next queue
@@ -126,7 +134,11 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
   const double E = 4.0 * kNnU32 * P.nn_cmax * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
   const float G = (float)(8.0 * kNnU32 * P.nn_cmax);  // box_lb32's coordinate shift
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
-  const float E32 = __double2float_ru(E * (1.0 + 1e-9)), ru32 = __double2float_ru(ru);
+#ifndef TCMP_NN_RWPAD
+#define TCMP_NN_RWPAD 0  // 1: pad the pruning threshold by the rewire radius (round 1)
+#endif
+  const float E32 = __double2float_ru(E * (1.0 + 1e-9)),
+              ru32 = TCMP_NN_RWPAD ? __double2float_ru(ru) : 0.f;
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
   unsigned long long pairs = 0, tests = 0;
 #ifdef TCMP_PROF
@@ -421,7 +433,7 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     const double sec = wave_min(mine);
     if (lane == 0) {
       nn[lj] = wi == INT_MAX ? 0 : wi;
-      if (second) second[lj] = sec;
+      if (second) second[lj] = TCMP_NN_RWPAD ? sec : fmin(sec, (double)thr);
       if (score) score[lj] = m;
     }
     NN_TICK(4);
