@@ -141,11 +141,23 @@ __global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long l
     for (int k = 0; k < 7; ++k) cand[8 * (size_t)j + k] = (1 - u[k]) * kLo[k] + u[k] * kHi[k];
   }
   cgoal[j] = 0;
-  const bool raw = st->goal_node < 0 && (it == 0 || u[7] < P.goal_prob);
-  // the round's lowest selecting lane: one atomic per wave (its lowest selecting lane -- lanes
-  // hold consecutive j), not one per selecting lane (a fifth of them while the goal is open)
+  if (st->goal_node >= 0) return;  // goal reached: no goal-biased lane (round_goal stays INT_MAX)
+  // The round's lowest selecting lane.  Every wave first evaluates the selection of lanes
+  // 0..63 (their Philox draws, one per lane): one of them selects with probability
+  // 1 - (1 - goal_prob)^64, and then that is the answer -- one plain store, instead of 4,096
+  // waves' atomics on one address (~40 us per round).  Otherwise each wave adds its lowest
+  // selecting lane with one atomic.
+  const int lane = lane_id();
+  double v[8];
+  philox_uniforms(P.seed, (uint64_t)(base + lane), v);
+  const uint64_t m0 = __ballot(lane < nb && (base + lane == 0 || v[7] < P.goal_prob));
+  if (m0) {
+    if (j == 0) st->round_goal = __builtin_ctzll(m0);
+    return;
+  }
+  const bool raw = it == 0 || u[7] < P.goal_prob;
   const uint64_t m = __ballot(raw);
-  if (m && lane_id() == __builtin_ctzll(m)) atomicMin(&st->round_goal, j);
+  if (m && lane == __builtin_ctzll(m)) atomicMin(&st->round_goal, j);
 }
 
 // ------------------------------------------------------------------------------------------
