@@ -1339,8 +1339,12 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(kNnBlock), 0, h->stream, dP, st, \
                      h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,          \
                      h->cperm.p, h->chome.p, nb, nn, second, score)
-  // four cells per scan round (eight measured slower: 137 VGPRs cost a wave per SIMD)
-  if (P.uniform_w) TCMP_NNW(true, 4); else TCMP_NNW(false, 4);
+  // two cells per scan round: same-box A/B of 1 / 2 / 3 / 4 / 5 gave 4.44 / 4.03 / 4.21 /
+  // 4.23 / 4.27 ms of scan per C3 query (eight: 137 VGPRs cost a wave per SIMD)
+#ifndef TCMP_NN_SW
+#define TCMP_NN_SW 2
+#endif
+  if (P.uniform_w) TCMP_NNW(true, TCMP_NN_SW); else TCMP_NNW(false, TCMP_NN_SW);
 #undef TCMP_NNW
   HIPCHK(hipGetLastError());
   const hipEvent_t e1 = h->mark_end(F_NNSCAN, e0);

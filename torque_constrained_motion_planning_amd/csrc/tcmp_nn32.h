@@ -100,7 +100,7 @@ constexpr int kNnBlock = 1024;
 #define TCMP_NN_LDS_SUP 1024
 #endif
 constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
-// SW: cells per scan round (4 or 8).  Passing cells queue up across super-cells (the queue
+// SW: cells per scan round (2 in the engine).  Passing cells queue up across super-cells (the queue
 // holds at most SW) and a round loads all their rows at once: fewer dependent round trips
 // per candidate than one round per super-cell.
 template <bool UW, int SW>
