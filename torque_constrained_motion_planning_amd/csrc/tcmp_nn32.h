@@ -156,7 +156,10 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
   // Candidates are taken kNnBatch at a time: one atomic per batch, the batch's cperm / home /
   // candidate rows loaded once by lanes 0..3, and the next batch's atomic issued before this
   // batch's work so its latency overlaps the first chunk loads.
-  constexpr int kNnBatch = 4;
+#ifndef TCMP_NN_BATCH
+#define TCMP_NN_BATCH 4
+#endif
+  constexpr int kNnBatch = TCMP_NN_BATCH;
   int qi = (int)xcc_id(), tried = 0;
   int jb = -1, jn = 0;
   auto grab_slow = [&]() {
