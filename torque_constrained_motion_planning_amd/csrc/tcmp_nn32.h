@@ -95,7 +95,10 @@ __device__ __forceinline__ float box_lb32(const float* b, const float sh[7], con
 // super-cell tests then cost an LDS round trip instead of an L2 one, and the block level (whose
 // only job is to save super-cell box loads) is skipped.  Larger indexes walk the blocks from
 // global memory as before.  (One walk over a flat pointer serving both was 5 % slower.)
-constexpr int kNnBlock = 1024;
+#ifndef TCMP_NN_BLOCK
+#define TCMP_NN_BLOCK 1024
+#endif
+constexpr int kNnBlock = TCMP_NN_BLOCK;
 #ifndef TCMP_NN_LDS_SUP
 #define TCMP_NN_LDS_SUP 1024
 #endif
@@ -104,7 +107,12 @@ constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
 // holds at most SW) and a round loads all their rows at once: fewer dependent round trips
 // per candidate than one round per super-cell.
 template <bool UW, int SW>
-__global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
+#ifdef TCMP_NN_WPE
+#define TCMP_NN_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TCMP_NN_WPE)))
+#else
+#define TCMP_NN_WPE_ATTR
+#endif
+__global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* stree32, const float* cbox,
                                                         const float* sbox, const float* bbox,
@@ -205,9 +213,11 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     float s32[7], sh[7], sl32[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
-      s32[k] = (float)s[k];
-      sh[k] = s32[k] + G;
-      sl32[k] = s32[k] - G;
+      // wave-uniform: readfirstlane puts them back in SGPRs (the VALU arithmetic leaves them
+      // in VGPRs otherwise, 21 registers the scan loop needs)
+      s32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)s[k])));
+      sh[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] + G)));
+      sl32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] - G)));
     }
     const int hc = __builtin_amdgcn_readlane(hml, ib);
     const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
