@@ -1326,10 +1326,10 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         count += (int)__popcll(bm);
       }
     }
+    // one flush call site (a full queue always holds pairs): phase B is inlined once
+    if (count) flush();
     if (!full) break;
-    flush();
   }
-  if (count) flush();
   __builtin_amdgcn_wave_barrier();
   coll |= active && ((*cmask >> lane) & 1ull);
   return coll;
