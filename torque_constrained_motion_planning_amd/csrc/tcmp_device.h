@@ -149,8 +149,17 @@ __host__ __device__ constexpr unsigned stage_lds_bytes(int n_obs) {
 // Mesh scenes (up to kMaxObstacles records, hull-vs-hull exact tests) stage only the fp32
 // tier-0 records and the pair queues, so that LDS does not cap residency at one 256-thread
 // block per CU; the fp64 records and the hull geometry are then read through the caches.
+// Behind the four pair queues, each wave of a mesh kernel parks its lanes' sin/cos (14 x 64
+// doubles) and the link poses of its pending exact pairs (12 x 64 doubles) in LDS, so that
+// neither stays in registers across the hull-vs-hull tests.
+constexpr unsigned kStashDoubles = 26 * 64;
 __host__ __device__ constexpr unsigned stage_lds_bytes_lean(int n_obs) {
-  return (unsigned)(n_obs > 0 ? n_obs : 1) * (8 * sizeof(float)) + 4 * kQwaveBytes;
+  return (unsigned)(n_obs > 0 ? n_obs : 1) * (8 * sizeof(float)) + 4 * kQwaveBytes +
+         4 * kStashDoubles * sizeof(double);
+}
+__device__ __forceinline__ double* wave_stash(unsigned* wq) {
+  const unsigned w = threadIdx.x >> 6;
+  return reinterpret_cast<double*>(wq + (4 - w) * (kQwaveBytes / 4)) + w * kStashDoubles;
 }
 template <bool FULL>
 __device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* lds, Scene& so,
@@ -1147,6 +1156,19 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
   __builtin_amdgcn_wave_barrier();
   int count = 0;  // wave-uniform
   const bool live = active && !coll;
+  // mesh kernels: cq / sq are read back from the wave's LDS stash (stored once here), so they
+  // are not live in registers across phase B; the clobber keeps the reads real loads
+  double* stash = MESH ? wave_stash(sc.wq) : nullptr;
+  if (MESH) {
+#pragma unroll
+    for (int k = 0; k < 7; ++k) {
+      stash[k * 64 + lane] = cq[k];
+      stash[(7 + k) * 64 + lane] = sq[k];
+    }
+    __asm__ volatile("" ::: "memory");
+  }
+  auto cq_of = [&](int k, int l) { return MESH ? stash[k * 64 + l] : __shfl(cq[k], l); };
+  auto sq_of = [&](int k, int l) { return MESH ? stash[(7 + k) * 64 + l] : __shfl(sq[k], l); };
   // ---- phase B ------------------------------------------------------------------------
   auto flush = [&]() {
     __builtin_amdgcn_wave_barrier();
@@ -1160,8 +1182,8 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       double c[7], s[7];
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
-        c[k] = __shfl(cq[k], src);
-        s[k] = __shfl(sq[k], src);
+        c[k] = cq_of(k, src);
+        s[k] = sq_of(k, src);
       }
       double R[9], p[3];
       link_pose(lk, c, s, R, p);
@@ -1196,6 +1218,16 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       }
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
+      if (MESH && pend) {
+        // the pending pairs' poses go to the stash: R / p die here instead of living across
+        // every hull-vs-hull test of the wave
+        double* ps = stash + 14 * 64;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) ps[k * 64 + lane] = R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ps[(9 + k) * 64 + lane] = p[k];
+        __asm__ volatile("" ::: "memory");
+      }
       while (pend) {
         const int L = __builtin_ctzll(pend);
         pend &= pend - 1;
@@ -1207,10 +1239,18 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         const int lL = __builtin_amdgcn_readfirstlane(__shfl(lk, L)),
                   oL = __builtin_amdgcn_readfirstlane(__shfl(orow, L));
         Pose PL;
+        if (MESH) {
+          const double* ps = stash + 14 * 64;
 #pragma unroll
-        for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
+          for (int k = 0; k < 9; ++k) PL.R[k] = ps[k * 64 + L];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) PL.p[k] = __shfl(p[k], L);
+          for (int k = 0; k < 3; ++k) PL.p[k] = ps[(9 + k) * 64 + L];
+        } else {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
+#pragma unroll
+          for (int k = 0; k < 3; ++k) PL.p[k] = __shfl(p[k], L);
+        }
         const double* ob = sc.obs + 16 * oL;
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
@@ -1252,7 +1292,8 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
-        const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
+        const double cr = kJcr[j], sr = kJsr[j], c = MESH ? stash[j * 64 + lane] : cq[j],
+                     s = MESH ? stash[(7 + j) * 64 + lane] : sq[j];
         const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
         const double t[3] = {kJx[j], kJy[j], kJz[j]};
         frame_step(R, p, Rl, t);
