@@ -825,12 +825,26 @@ namespace tcmp {
 // it) and against its inner box ("collision" at kPen + guard and above, it lies inside the
 // mesh) -- both hull-vs-box -- then the hull-vs-hull test.  fp32 first, fp64 near kPen.
 template <bool MESH>
-__device__ __forceinline__ double exact_pair(int link, const Pose PL, const double* ob,
-                                             const Scene sc, const Geo g) {
+__device__ __forceinline__ double exact_pair(int link, const Pose PL0, const double* ps,
+                                             const double* ob, const Scene sc, const Geo g) {
   const int mi = MESH ? obs_mesh(ob) : -1;
+  // mesh kernels: the pose is re-read from the wave's LDS stash (ps: its column, stride 64) at
+  // each use instead of living in 24 VGPRs across the hull-vs-hull tests; the clobber keeps
+  // the re-reads from being merged
+  auto pose = [&]() -> Pose {
+    if (!MESH) return PL0;
+    __asm__ volatile("" ::: "memory");
+    Pose x;
+#pragma unroll
+    for (int k = 0; k < 9; ++k) x.R[k] = ps[k * 64];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) x.p[k] = ps[(9 + k) * 64];
+    return x;
+  };
   // the fp64 restatements are out of line; the pose reaches them through the wave's LDS slot
   auto pose_to_lds = [&]() {
     double* slot = wave_pose_slot(sc.wq);
+    const Pose PL = pose();
     if (lane_id() == 0) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) slot[k] = PL.R[k];
@@ -841,7 +855,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
     return (const double*)slot;
   };
   if (!MESH || mi < 0) {
-    const float pd32 = exact_pd_wave32(link, PL, ob, g);
+    const float pd32 = exact_pd_wave32(link, pose(), ob, g);
     if (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) return (double)pd32;
     return exact_pd_wave(link, pose_to_lds(), ob, g.verts, g.planes, g.edges);
   }
@@ -856,14 +870,17 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
-  const float po = exact_pd_wave32(link, PL, ob, g);
+  const float po = exact_pd_wave32(link, pose(), ob, g);
   TCMP_MESH_CLK(0);
   if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
   float R[9], p[3];
+  {
+    const Pose PL = pose();
 #pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = (float)PL.R[k];
+    for (int k = 0; k < 9; ++k) R[k] = (float)PL.R[k];
 #pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = (float)PL.p[k];
+    for (int k = 0; k < 3; ++k) p[k] = (float)PL.p[k];
+  }
   if (rg[18]) {
     // level-of-detail certificates: outer LODs contain the hulls ("free" below kPen - guard),
     // inner LODs lie inside them ("collision" above kPen + guard)
@@ -886,7 +903,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL, const doub
   } else {
     const double* ib = sc.mib + 16 * mi;
     if (ib[12] > 0.0) {
-      const float pi = exact_pd_wave32(link, PL, ib, g);
+      const float pi = exact_pd_wave32(link, pose(), ib, g);
       if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
     }
   }
@@ -1239,13 +1256,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         const int lL = __builtin_amdgcn_readfirstlane(__shfl(lk, L)),
                   oL = __builtin_amdgcn_readfirstlane(__shfl(orow, L));
         Pose PL;
-        if (MESH) {
-          const double* ps = stash + 14 * 64;
-#pragma unroll
-          for (int k = 0; k < 9; ++k) PL.R[k] = ps[k * 64 + L];
-#pragma unroll
-          for (int k = 0; k < 3; ++k) PL.p[k] = ps[(9 + k) * 64 + L];
-        } else {
+        if (!MESH) {
 #pragma unroll
           for (int k = 0; k < 9; ++k) PL.R[k] = __shfl(R[k], L);
 #pragma unroll
@@ -1255,7 +1266,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
 #endif
-        const double pd = exact_pair<MESH>(lL, PL, ob, sc, g);
+        const double pd = exact_pair<MESH>(lL, PL, MESH ? stash + 14 * 64 + L : nullptr, ob, sc, g);
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif
