@@ -132,6 +132,7 @@ def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None, n_me
 
 
 HOST_MS = {"begin": 0.0, "run": 0.0, "finish": 0.0, "fetch": 0.0}  # host wall time per call
+GATHER = {"ok": True, "queries": 0, "rows": 0}  # rank 0's checks of the timed steps' gathers
 
 
 def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass=5.0,
@@ -158,6 +159,26 @@ def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass
     for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
         HOST_MS[k] += (b - a) * 1e3
     return r, out
+
+
+def usable_cores():
+    """CPUs this process may actually run on: the affinity mask, capped by a cgroup v2 CPU
+    quota (a GPU box shares its host: nproc counts the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
+def log(msg):
+    print("[bench %.0fs] %s" % (time.perf_counter() - T_START, msg), file=sys.stderr, flush=True)
+
+
+T_START = time.perf_counter()
 
 
 def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=None,
@@ -192,9 +213,18 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
         dtw = time.perf_counter() - t0
         done = [json.loads(o) for o, p in zip(outs, procs) if p.returncode == 0 and o.strip()]
     multi = sum(d["samples"] for d in done) / dtw if done else None
+    nproc = os.cpu_count() or 1
+    per_core = multi / len(done) if multi else single
+    log("cpu baseline: %d workers, %.0f samples/s" % (len(done), multi or single))
     return {"value": multi if multi else single, "unit": "samples/s",
-            "cores": len(done) if multi else 1, "host_nproc": os.cpu_count(), "kind": "port",
+            "cores": len(done) if multi else 1, "host_nproc": nproc,
+            "usable_cores": usable_cores(), "kind": "port",
             "single_core": single,
+            # SURVEY 8d asks for all host cores: the measured per-core rate scaled to nproc
+            # (a shared GPU box lets this process use only its share of them), and one GPU's
+            # share of an 8-GPU node's host cores
+            "all_cores_scaled": {"cores": nproc, "value": per_core * nproc},
+            "per_gpu_share": {"cores": nproc / 8.0, "value": per_core * nproc / 8.0},
             "sample": "oracle/tcmp_oracle.c sequential RRT* (B=1, reference loop semantics) on the "
                       "same %s: %d samples per query; single core "
                       "%.1f s (%d nodes, %d extend steps); %d independent queries, one per core, "
@@ -213,8 +243,11 @@ def main():
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--obstacles", type=int, default=None, help="boxes per scene")
     ap.add_argument("--cpu-samples", type=int, default=40000)
-    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1),
-                    help="host cores for the multi-core CPU baseline (16 = one GPU's share)")
+    ap.add_argument("--cpu-workers", type=int, default=usable_cores(),
+                    help="worker processes of the multi-core CPU baseline (default: every "
+                         "core this process may use -- affinity and cgroup quota; the all-core "
+                         "and per-GPU (nproc/8) figures are the measured per-core rate scaled "
+                         "to the host's nproc, reported beside it)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the SURVEY 8d default-batch line (config_alt)")
@@ -261,9 +294,11 @@ def main():
     if W["queries"] > 1:
         qids = shard.queries_for_rank(W["queries"], world, rank)
         labels = list(qids)
+        all_labels = list(range(W["queries"]))
     else:
         qids = [0]
         labels = [rank]
+        all_labels = list(range(world))
     eng.set_self_collision(args.self_collisions)
     queries = [make_query(1234 + q, n_obs=W["boxes"], mode=mode, mass=mass, engine=eng,
                           n_mesh=W["meshes"]) for q in qids]
@@ -305,22 +340,36 @@ def main():
         outs = [d[2] for d in done]
         res = [d[1].as_dict() for d in done]
         if comm is not None and not shared:
-            # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3])
-            shard.gather_trajectories(comm, [shard.pack_trajectory(o) for o in outs], labels)
+            # RCCL gather of the solved trajectories (q, qd, qdd, dt) to rank 0 (configs[3]),
+            # checked on rank 0: every rank's query ids arrived, row counts as all-gathered
+            trajs = [shard.pack_trajectory(o) for o in outs]
+            sizes = comm.allgather_i64([len(labels), sum(len(t) for t in trajs)])
+            ids, rows, data = shard.pack_paths(trajs, labels)
+            got = comm.gather_paths(ids, rows, data, int(sizes[:, 0].sum()),
+                                    int(sizes[:, 1].sum()), sizes=sizes)
+            if rank == 0:
+                got = shard.unpack_paths(*got)
+                GATHER["ok"] &= shard.gather_ok(got, all_labels, sizes)
+                GATHER["queries"] += len(got)
+                GATHER["rows"] += int(sizes[:, 1].sum())
         return res
 
+    log("workload %s ready on rank %d of %d" % (args.workload, rank, world))
     for w in range(args.warmup):
         step(10_000 + w)
+    log("warmup done")
 
     barrier()
     for k in HOST_MS:
         HOST_MS[k] = 0.0
+    GATHER.update(ok=True, queries=0, rows=0)
     t0 = time.perf_counter()
     results = []
     for s in range(args.steps):
         results += step(s)
     barrier()
     dt = time.perf_counter() - t0
+    log("timed steps done: %.3f s" % dt)
     # samples the devices actually drew (tcmp_plan_result.n_samples), summed over all ranks
     total_samples = float(sum(x["n_samples"] for x in results))
     if comm is not None:
@@ -409,6 +458,14 @@ def main():
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},
     }
+    if comm is not None:
+        # proof of the collective world the run used: RCCL's own rank count, and rank 0's check
+        # that every gather delivered every query id with the all-gathered row counts
+        line["rccl_ranks"] = comm.rccl_ranks()
+        if not shared:
+            line["gather_ok"] = bool(GATHER["ok"])
+            line["gathered"] = {"queries": GATHER["queries"], "rows": GATHER["rows"],
+                                "steps": S}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         obs, pack, goal = queries[0]
         cpu_n = args.cpu_samples if not W["meshes"] else max(1000, args.cpu_samples // 10)

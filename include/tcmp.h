@@ -113,6 +113,18 @@ int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const doub
  * link hull vs every obstacle, penetration >= 0.04 m.  collides: n int32. */
 int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* collides);
 
+/* Body-level check any(pairwise_collision(robot, b) for b in obstacles) on n configurations
+ * (franka_ik_fast.py:78, panda_primitives.py:260 -> utils.py:2872-2880 body_collision ->
+ * get_closest_points(max_distance=-0.04), :2833): every link of the robot body, i.e. the moving
+ * links AND the static base panda_link0, penetration >= 0.04 m, no joint-limit test.
+ * collides: n int32. */
+int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collides);
+
+/* Penetration depth of the static base panda_link0 (world = base frame) against each obstacle
+ * of the scene: the tcmp_set_scene boxes, then the tcmp_set_meshes meshes (n must be their
+ * sum).  The q-independent half of tcmp_check_body. */
+int tcmp_base_pd(tcmp_handle* h, double* pd, int32_t n);
+
 /* safe_path_force_aware(extend(from, to), collision, torque) for n edges (rrt_star.py:90-98,
  * utils.py:3068-3077 with the given resolution vector (7, NULL = 0.1 as the planner uses)).
  * n_safe = len(safe prefix), n_steps = len(extend), last = prefix[-1] (valid if n_safe>0). */
@@ -256,8 +268,11 @@ int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn
 #define TCMP_REDUCE_SUM 0
 #define TCMP_REDUCE_MAX 1
 
-/* TCP rendezvous: rank 0 listens on addr:port and sends its nbytes `blob` to every other
- * rank (which connect, retrying until timeout_ms).  Host only, no GPU.  Used for the
+/* TCP rendezvous: rank 0 listens on addr:port; every other rank connects (retrying until
+ * timeout_ms) and introduces itself with the job's identity (TCMP_JOB_ID, else the launcher's
+ * TORCHELASTIC_RUN_ID, hashed with world and port: a stale or concurrent job is turned away).
+ * Rank 0 sends its nbytes `blob` only after all world - 1 ranks have arrived; on a timeout it
+ * closes every connection, so every rank fails together.  Host only, no GPU.  Used for the
  * ncclUniqueId; world == 1 returns at once. */
 int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port, void* blob,
                     int32_t nbytes, int32_t timeout_ms);
@@ -268,6 +283,9 @@ int tcmp_dist_init(int32_t rank, int32_t world, int32_t device, const char* addr
                    tcmp_comm** out);
 int tcmp_dist_destroy(tcmp_comm* c);
 int tcmp_dist_rank(const tcmp_comm* c, int32_t* rank, int32_t* world);
+/* ranks of the communicator's RCCL handle (ncclCommCount); 0 for a one-rank job, which has
+ * no RCCL communicator.  Lets a multi-GPU run prove which collective world it ran in. */
+int tcmp_dist_rccl_ranks(const tcmp_comm* c, int32_t* n);
 /* device-synchronise this rank, then an RCCL all-reduce as the barrier */
 int tcmp_dist_barrier(tcmp_comm* c);
 /* in-place all-reduce of n doubles (op TCMP_REDUCE_SUM / TCMP_REDUCE_MAX) */
@@ -276,14 +294,24 @@ int tcmp_dist_allreduce(tcmp_comm* c, double* v, int32_t n, int32_t op);
 int tcmp_dist_allgather_i64(tcmp_comm* c, const int64_t* in, int32_t n, int64_t* out);
 
 /* gather every rank's solved paths to rank 0 (ncclGroupStart; ncclSend/ncclRecv;
- * ncclGroupEnd after a size all-gather).  In: n_local paths, ids[i], rows[i], data = the
- * paths' rows concatenated (sum(rows) x TCMP_TRAJ_COLS).  Out, rank 0 only: n_queries paths
- * in rank order (out_ids, out_rows) with their rows concatenated in out_data; elsewhere
- * n_queries = n_rows = 0.  Capacities too small: status -4 with n_queries / n_rows set (the
- * collective still completes on every rank).  Collective: every rank must call it. */
+ * ncclGroupEnd).  In: n_local paths, ids[i], rows[i], data = the paths' rows concatenated
+ * (sum(rows) x TCMP_TRAJ_COLS); sizes = world x 2 int64 (queries, rows) of every rank when the
+ * caller has all-gathered them already (tcmp_dist_allgather_i64), else NULL and the call does
+ * the size all-gather itself.  Out, rank 0 only: n_queries paths in rank order (out_ids,
+ * out_rows) with their rows concatenated in out_data, laid out by tcmp_gather_layout;
+ * elsewhere n_queries = n_rows = 0.  Capacities too small: status -4 with n_queries / n_rows
+ * set (the collective still completes on every rank).  Collective: every rank must call it.
+ * Replaces the reference's host loop over queries (collect_data.py:74-85). */
 int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const int64_t* rows,
-                      const double* data, int64_t cap_queries, int64_t cap_rows, int64_t* out_ids,
-                      int64_t* out_rows, double* out_data, int64_t* n_queries, int64_t* n_rows);
+                      const double* data, const int64_t* sizes, int64_t cap_queries,
+                      int64_t cap_rows, int64_t* out_ids, int64_t* out_rows, double* out_data,
+                      int64_t* n_queries, int64_t* n_rows);
+
+/* rank 0's receive layout of tcmp_gather_paths, host only: from sizes (world x 2: queries,
+ * rows per rank) each rank's first header row q_off[k] and first trajectory row r_off[k] in
+ * the rank-ordered output, and the totals.  Any output pointer may be NULL. */
+int tcmp_gather_layout(int32_t world, const int64_t* sizes, int64_t* q_off, int64_t* r_off,
+                       int64_t* total_q, int64_t* total_r);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,8 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+# ORC_LIB_PATH: another build of the same sources (the sanitizer build, `make -C oracle asan`)
+LIB_PATH = os.environ.get("ORC_LIB_PATH", os.path.join(HERE, "build", "liboracle.so"))
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -70,6 +71,10 @@ def lib():
         L.orc_self_pair_pd.argtypes = [ctypes.c_int, ctypes.c_int, _dp, ctypes.c_int]
         L.orc_self_pair_pd.restype = ctypes.c_double
         L.orc_nearest.argtypes = [_dp, ctypes.c_long, _dp, ctypes.c_long, _dp, _ip, _dp]
+        L.orc_set_threads.argtypes = [ctypes.c_int]
+        L.orc_base_pd.argtypes = [_dp, ctypes.c_int, _dp]
+        L.orc_body_collision.argtypes = [_dp, _dp, ctypes.c_int, ctypes.c_int]
+        L.orc_set_tree_out.argtypes = [_dp, _dp, _ip, ctypes.c_long]
         L.orc_rrt_run.argtypes = [ctypes.POINTER(RrtCfg), ctypes.POINTER(RrtResult), _dp,
                                   ctypes.c_long, _dp, _dp, _dp, _dp, ctypes.c_long]
         assert L.orc_sizeof_cfg() == ctypes.sizeof(RrtCfg), "oracle cfg layout mismatch"
@@ -141,6 +146,24 @@ def collision(q, obs, cull=1):
     q = _arr(q, (7,))
     o = obstacles_array(obs)
     return bool(lib().orc_collision(_d(q), _d(o) if len(o) else None, len(o), int(cull)))
+
+
+def body_collision(q, obs, cull=1):
+    """pairwise_collision(robot, b) over every obstacle b: all robot links, the static base
+    panda_link0 included, at the -0.04 threshold, no joint-limit test."""
+    o = obstacles_array(obs)
+    return bool(lib().orc_body_collision(_d(_arr(q, (7,))), _d(o) if len(o) else None, len(o),
+                                         int(cull)))
+
+
+def base_pd(obs):
+    """panda_link0's penetration depth against each box of `obs`, then each mesh set by
+    set_meshes."""
+    o = obstacles_array(obs)
+    out = np.zeros(len(o) + lib().orc_mesh_count())
+    if len(out):
+        lib().orc_base_pd(_d(o) if len(o) else None, len(o), _d(out))
+    return out
 
 
 def pair_pd(link, q, box, method=0):
@@ -252,8 +275,11 @@ def philox_uniforms(seed, k):
 def rrt_run(start, goal, max_samples, obs=None, torque_mode=0, mass=0.0, exec_time=5.0,
             batch=1, seed=0, replay_random=None, replay_uniform=None, radius=0.01,
             goal_prob=0.2, goal_tol=1e-2, cull=1, validate=True, cap_wp=1 << 16,
-            cap_traj=1 << 20, informed=False):
-    """Runs the restated RRT*; returns dict with status, counters, waypoints, traj."""
+            cap_traj=1 << 20, informed=False, threads=1, tree=False):
+    """Runs the restated RRT*; returns dict with status, counters, waypoints, traj.
+    threads > 1 runs the per-lane loops of a round (nearest, edges, rewire scans) on that
+    many OpenMP threads; results do not depend on it (used for bench-size fixtures).
+    tree=True also returns the final tree ("tree_cfg", "tree_cost", "tree_parent")."""
     cfg = RrtCfg()
     cfg.start[:] = list(map(float, start)); cfg.goal[:] = list(map(float, goal))
     cfg.max_samples = int(max_samples); cfg.batch = int(batch); cfg.torque_mode = int(torque_mode)
@@ -276,12 +302,26 @@ def rrt_run(start, goal, max_samples, obs=None, torque_mode=0, mass=0.0, exec_ti
     wp = np.zeros((cap_wp, 7))
     tq = np.zeros((cap_traj, 7)); tqd = np.zeros_like(tq); tqdd = np.zeros_like(tq)
     psg = np.zeros(cap_traj)
-    lib().orc_rrt_run(ctypes.byref(cfg), ctypes.byref(res), _d(wp), cap_wp, _d(tq), _d(tqd),
-                      _d(tqdd), _d(psg), cap_traj)
+    lib().orc_set_threads(int(threads))
+    if tree:
+        cap_n = int(max_samples) + 1
+        t_cfg = np.zeros((cap_n, 7)); t_cost = np.zeros(cap_n)
+        t_par = np.zeros(cap_n, dtype=np.int32)
+        lib().orc_set_tree_out(_d(t_cfg), _d(t_cost), t_par.ctypes.data_as(_ip), cap_n)
+    try:
+        lib().orc_rrt_run(ctypes.byref(cfg), ctypes.byref(res), _d(wp), cap_wp, _d(tq), _d(tqd),
+                          _d(tqdd), _d(psg), cap_traj)
+    finally:
+        lib().orc_set_threads(1)
+        if tree:
+            lib().orc_set_tree_out(None, None, None, 0)
     out = {f: getattr(res, f) for f, _ in RrtResult._fields_}
     W = res.n_waypoints
     K = res.n_traj
     out["waypoints"] = wp[:W].copy()
     out["q"] = tq[:K].copy(); out["qd"] = tqd[:K].copy(); out["qdd"] = tqdd[:K].copy()
     out["psg"] = psg[:K].copy()
+    if tree:
+        n = res.n_nodes
+        out["tree_cfg"] = t_cfg[:n]; out["tree_cost"] = t_cost[:n]; out["tree_parent"] = t_par[:n]
     return out

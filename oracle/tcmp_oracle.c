@@ -22,6 +22,7 @@
 #include <string.h>
 
 #include "../torque_constrained_motion_planning_amd/csrc/panda_geometry.inc"
+#include "../torque_constrained_motion_planning_amd/csrc/panda_base.inc"
 
 #define ORC_API __attribute__((visibility("default")))
 
@@ -790,7 +791,7 @@ static double hull_pd_brute(const orc_whull* Ap, const double* Bv, int nvb, cons
 }
 
 ORC_API double orc_hull_mesh_pd_brute(int link, const double* fr, int m) {
-  static orc_whull A;
+  static _Thread_local orc_whull A;
   link_world_hull(link, fr, &A);
   return hull_pd_brute(&A, g_mesh.v + 3 * g_mesh.voff[m], g_mesh.voff[m + 1] - g_mesh.voff[m],
                        g_mesh.pl + 4 * g_mesh.poff[m], g_mesh.poff[m + 1] - g_mesh.poff[m],
@@ -850,7 +851,7 @@ static double hull_pd_gauss(const orc_whull* Ap, const double* Bv, int nvb, cons
 }
 
 ORC_API double orc_hull_mesh_pd_gauss(int link, const double* fr, int m) {
-  static orc_whull A;
+  static _Thread_local orc_whull A;
   link_world_hull(link, fr, &A);
   return hull_pd_gauss(&A, g_mesh.v + 3 * g_mesh.voff[m], g_mesh.voff[m + 1] - g_mesh.voff[m],
                        g_mesh.pl + 4 * g_mesh.poff[m], g_mesh.poff[m + 1] - g_mesh.poff[m],
@@ -870,6 +871,14 @@ static const int kBodyArmJoint[ORC_BODY_LINKS] = {1, 1, 1, 1, 1, 1, 1, 0, 0, 0, 
 static const int kBodyColl[ORC_BODY_LINKS] = {0, 1, 2, 3, 4, 5, 6, -1, 7, 8, 9, -1};
 
 static int g_self = 0;
+/* worker threads of orc_rrt_run's per-lane loops (test fixtures at bench size only) */
+static int g_threads = 1;
+ORC_API void orc_set_threads(int n) { g_threads = n > 0 ? n : 1; }
+/* optional copy of the final tree (configs, costs, parents) for fixtures */
+static struct { double* cfg; double* cost; int* parent; long cap; } g_tree_out;
+ORC_API void orc_set_tree_out(double* cfg, double* cost, int* parent, long cap) {
+  g_tree_out.cfg = cfg; g_tree_out.cost = cost; g_tree_out.parent = parent; g_tree_out.cap = cap;
+}
 ORC_API void orc_set_self_collision(int on) { g_self = on ? 1 : 0; }
 
 /* moving arm joints among a link's ancestors, itself included (get_joint_ancestors & joints) */
@@ -919,7 +928,7 @@ static int orc_self_pair_collides(int a, const double* fa, int b, const double* 
     if (obb_obb_pd(ba, ba + 3, ba + 12, cl, A, wb + 12) < ORC_PEN) return 0;
     if (ba[15] > 0 && bb[15] > 0 && obb_obb_pd(ba, ba + 3, ba + 15, cl, A, wb + 15) >= ORC_PEN) return 1;
   }
-  static orc_whull A, B;
+  static _Thread_local orc_whull A, B;
   link_world_hull(a, fa, &A);
   link_world_hull(b, fb, &B);
   const double pd = cull == 2 ? hull_pd_gauss(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne)
@@ -931,7 +940,7 @@ static int orc_self_pair_collides(int a, const double* fa, int b, const double* 
 ORC_API double orc_self_pair_pd(int a, int b, const double* q, int method) {
   double fr[120];
   orc_fk_links(q, fr);
-  static orc_whull A, B;
+  static _Thread_local orc_whull A, B;
   link_world_hull(a, fr + 12 * a, &A);
   link_world_hull(b, fr + 12 * b, &B);
   return method == 1 ? hull_pd_gauss(&A, B.v, B.nv, B.pl, B.nf, B.e, B.ne)
@@ -966,8 +975,85 @@ ORC_API double orc_mesh_pair_pd(int link, const double* q, int m, int method) {
  * Self-collision pairs only after orc_set_self_collision(1) (off in the reference planner,
  * utils.py:56 SELF_COLLISIONS=False), no attachments.  Convex meshes
  * (orc_set_meshes) after the boxes. */
+static int orc_links_collide(const double* q, const double* obs, int n_obs, int cull);
 ORC_API int orc_collision(const double* q, const double* obs, int n_obs, int cull) {
   if (orc_limits_violated(q)) return 1;
+  return orc_links_collide(q, obs, n_obs, cull);
+}
+
+/* ------------------------------------------------------------------------------------ */
+/* Body-level check (pairwise_collision(robot, b), utils.py:2872-2880 -> body_collision    */
+/* :2866 -> get_closest_points(max_distance=-MAX_DISTANCE) :2833): every link of the robot */
+/* body against obstacle b at the same -0.04 threshold, no joint-limit test.  Used on the  */
+/* grasp configuration (franka_ik_fast.py:78, panda_primitives.py:260).  Beyond the moving */
+/* links it covers the static base panda_link0 (panda_base.inc, base = world frame).       */
+/* ------------------------------------------------------------------------------------ */
+static void base_hull(orc_whull* H) {
+  H->nv = TCMP_BASE_NV; H->nf = TCMP_BASE_NF; H->ne = TCMP_BASE_NE;
+  for (int i = 0; i < H->nv; ++i)
+    for (int k = 0; k < 3; ++k) H->v[3 * i + k] = tcmp_base_verts[4 * i + k];
+  for (int i = 0; i < 4 * H->nf; ++i) H->pl[i] = tcmp_base_planes[i];
+  for (int i = 0; i < 4 * H->ne; ++i) H->e[i] = tcmp_base_edges[i];
+}
+
+/* an obstacle box record (c, R row-major with columns = axes, half) as a hull */
+static void box_hull(const double* ob, double v[24], double pl[24], int e[48]) {
+  const double* c = ob;
+  const double* R = ob + 3;
+  const double* h = ob + 12;
+  for (int i = 0; i < 8; ++i) {
+    const double s[3] = {(i & 1) ? 1.0 : -1.0, (i & 2) ? 1.0 : -1.0, (i & 4) ? 1.0 : -1.0};
+    for (int k = 0; k < 3; ++k)
+      v[3 * i + k] = c[k] + R[3 * k] * s[0] * h[0] + R[3 * k + 1] * s[1] * h[1] + R[3 * k + 2] * s[2] * h[2];
+  }
+  for (int a = 0; a < 3; ++a)
+    for (int sg = 0; sg < 2; ++sg) {
+      double* p = pl + 4 * (2 * a + sg);
+      const double sgn = sg ? -1.0 : 1.0;
+      for (int k = 0; k < 3; ++k) p[k] = sgn * R[3 * k + a];
+      p[3] = sgn * (c[0] * R[a] + c[1] * R[3 + a] + c[2] * R[6 + a]) + h[a];
+    }
+  /* 12 edges: vertex pairs differing in one sign bit (face indices unused by the brute force) */
+  int n = 0;
+  for (int i = 0; i < 8; ++i)
+    for (int a = 0; a < 3; ++a)
+      if (!(i & (1 << a))) {
+        e[4 * n] = i; e[4 * n + 1] = i | (1 << a); e[4 * n + 2] = 0; e[4 * n + 3] = 0;
+        ++n;
+      }
+}
+
+/* penetration depth of panda_link0 against each obstacle: the boxes, then the meshes set by
+ * orc_set_meshes (brute-force SAT over both hulls' facets and every edge pair) */
+ORC_API void orc_base_pd(const double* obs, int n_obs, double* pd) {
+  static _Thread_local orc_whull A;
+  base_hull(&A);
+  for (int o = 0; o < n_obs; ++o) {
+    double v[24], pl[24];
+    int e[48];
+    box_hull(obs + 15 * o, v, pl, e);
+    pd[o] = hull_pd_brute(&A, v, 8, pl, 6, e, 12);
+  }
+  for (int m = 0; m < g_mesh.n; ++m)
+    pd[n_obs + m] = hull_pd_brute(&A, g_mesh.v + 3 * g_mesh.voff[m], g_mesh.voff[m + 1] - g_mesh.voff[m],
+                                  g_mesh.pl + 4 * g_mesh.poff[m], g_mesh.poff[m + 1] - g_mesh.poff[m],
+                                  g_mesh.e + 4 * g_mesh.eoff[m], g_mesh.eoff[m + 1] - g_mesh.eoff[m]);
+}
+
+ORC_API int orc_body_collision(const double* q, const double* obs, int n_obs, int cull) {
+  if (orc_links_collide(q, obs, n_obs, cull)) return 1;
+  const int n = n_obs + g_mesh.n;
+  if (n <= 0) return 0;
+  double* pd = malloc(sizeof(double) * (size_t)n);
+  orc_base_pd(obs, n_obs, pd);
+  int hit = 0;
+  for (int i = 0; i < n; ++i) hit |= pd[i] >= ORC_PEN;
+  free(pd);
+  return hit;
+}
+
+/* every moving link against every obstacle (and the self pairs when on); no limits */
+static int orc_links_collide(const double* q, const double* obs, int n_obs, int cull) {
   if (n_obs <= 0 && g_mesh.n <= 0 && !g_self) return 0;
   double fr[120];
   orc_fk_links(q, fr);
@@ -1197,7 +1283,11 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
       }
     }
     long Tr = T.n;
+    /* The lanes of a round are independent until insertion (each sees the snapshot), so
+     * the nearest scans, the edges and the rewire-neighbour scans may run on several
+     * threads (orc_set_threads; default 1).  Insertion stays sequential in lane order. */
     /* nearest (rrt_star.py:9-14,171): argmin of distance, first index wins ties */
+#pragma omp parallel for schedule(dynamic, 64) num_threads(g_threads) if (g_threads > 1)
     for (int j = 0; j < nb; ++j) {
       double best = INFINITY;
       int bi = 0;
@@ -1208,8 +1298,34 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
       nn[j] = bi;
     }
     /* extend + safe path (rrt_star.py:172) */
-    for (int j = 0; j < nb; ++j)
-      nsafe[j] = orc_edge(&C, T.cfg + 7 * (long)nn[j], S + 7 * j, &ns[j], last + 7 * j);
+    {
+      long steps = 0;
+#pragma omp parallel for schedule(dynamic, 16) num_threads(g_threads) if (g_threads > 1) reduction(+ : steps)
+      for (int j = 0; j < nb; ++j) {
+        orc_ctx Cj = C;
+        Cj.edge_steps = 0;
+        nsafe[j] = orc_edge(&Cj, T.cfg + 7 * (long)nn[j], S + 7 * j, &ns[j], last + 7 * j);
+        steps += Cj.edge_steps;
+      }
+      C.edge_steps += steps;
+    }
+    /* rewire neighbours of each accepted node among the snapshot nodes (:183-186): the
+     * scan depends only on the node's configuration, so it runs before the insertion */
+    int* rwn = calloc((size_t)nb, sizeof(int));
+    int** rwl = calloc((size_t)nb, sizeof(int*));
+#pragma omp parallel for schedule(dynamic, 64) num_threads(g_threads) if (g_threads > 1)
+    for (int j = 0; j < nb; ++j) {
+      if (nsafe[j] == 0) continue;
+      int cnt = 0, cap = 0;
+      int* lst = 0;
+      for (long n = 0; n < Tr; ++n) {
+        double dn = orc_dist(T.cfg + 7 * n, last + 7 * j, C.w);
+        if (!(dn < cfg->radius)) continue;
+        if (cnt == cap) { cap = cap ? 2 * cap : 8; lst = realloc(lst, sizeof(int) * cap); }
+        lst[cnt++] = (int)n;
+      }
+      rwn[j] = cnt; rwl[j] = lst;
+    }
     /* insert in lane order + goal test + rewire against the round snapshot (:173-192) */
     for (int j = 0; j < nb; ++j) {
       if (nsafe[j] == 0) continue;
@@ -1218,7 +1334,8 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
       tree_push(&T, last + 7 * j, T.cost[par] + d, par, S + 7 * j, ns[j], nsafe[j]);
       long nw = T.n - 1;
       if (dog[j] && goal_n < 0 && orc_dist(T.cfg + 7 * nw, cfg->goal, C.w) < cfg->goal_tol) goal_n = nw;
-      for (long n = 0; n < Tr; ++n) {
+      for (int ii = 0; ii < rwn[j]; ++ii) {
+        long n = rwl[j][ii];
         double dn = orc_dist(T.cfg + 7 * n, T.cfg + 7 * nw, C.w);
         if (!(dn < cfg->radius)) continue;
         if (T.cost[n] + dn < T.cost[nw]) {
@@ -1235,11 +1352,18 @@ ORC_API int orc_rrt_run(const orc_rrt_cfg* cfg, orc_rrt_result* res, double* wp,
           }
         }
       }
+      free(rwl[j]);
     }
+    free(rwn); free(rwl);
     k += nb;
   }
   res->n_samples = k;
   res->n_nodes = T.n;
+  if (g_tree_out.cfg && T.n <= g_tree_out.cap) {
+    memcpy(g_tree_out.cfg, T.cfg, sizeof(double) * 7 * (size_t)T.n);
+    memcpy(g_tree_out.cost, T.cost, sizeof(double) * (size_t)T.n);
+    memcpy(g_tree_out.parent, T.parent, sizeof(int) * (size_t)T.n);
+  }
   res->goal_node = goal_n;
   res->edge_steps = C.edge_steps;
   if (goal_n < 0) { res->status = 2; goto done; }

@@ -4,6 +4,9 @@
   processes;
 * tcmp_gather_paths' packing and unpacking through the C-ABI (a one-rank communicator needs
   no RCCL and touches no GPU);
+* rank 0's receive layout of tcmp_gather_paths (tcmp_gather_layout) and the staging / unpacking
+  around it at world sizes 2..8, ragged;
+* the two-phase rendezvous failing on every rank together (a missing rank, another job);
 * the 2-rank shard path: round-robin deal, per-rank planning (the CPU oracle stands in for the
   GPU engine), the wire form of tcmp_gather_paths, with gloo moving the packed buffers the
   way RCCL's send/recv does on the GPU -- torch appears only in this test harness.
@@ -91,6 +94,10 @@ def _plan(O, qid):
 
 
 def _shard_worker(rank, world, port, n_queries, q):
+    """One rank of the shard path: round-robin deal, planning (the oracle stands in for the
+    engine), shard.pack_paths, the size all-gather, and rank 0's staging of every rank's
+    contribution at tcmp_gather_layout's offsets (shard.stage_rank0).  gloo only carries the
+    packed buffers between the processes -- RCCL's ncclSend/ncclRecv on the GPU."""
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import torch
@@ -103,29 +110,93 @@ def _shard_worker(rank, world, port, n_queries, q):
     ids_local = shard.queries_for_rank(n_queries, world, rank)
     ids, rows, data = shard.pack_paths([shard.pack_trajectory(_plan(O, i)) for i in ids_local],
                                        ids_local)
-    # tcmp_gather_paths' exchange: sizes all-gathered, then each rank's header and body to 0
     sizes = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
     dist.all_gather(sizes, torch.tensor([len(ids), int(rows.sum())], dtype=torch.int64))
-    hdr = torch.from_numpy(np.stack([ids, rows], 1).reshape(-1).copy())
-    body = torch.from_numpy(data.reshape(-1).copy())
+    sizes = torch.stack(sizes).numpy()
     if rank == 0:
-        hs, bs = [hdr], [body]
+        packed = [(ids, rows, data)]
         for r in range(1, world):
             nq, nr = (int(x) for x in sizes[r])
             h = torch.zeros(2 * nq, dtype=torch.int64)
             b = torch.zeros(22 * nr, dtype=torch.float64)
             dist.recv(h, src=r)
             dist.recv(b, src=r)
-            hs.append(h)
-            bs.append(b)
-        H = torch.cat(hs).numpy().reshape(-1, 2)
-        got = shard.unpack_paths(H[:, 0], H[:, 1], torch.cat(bs).numpy().reshape(-1, 22))
-        q.put(got)
+            hh = h.numpy().reshape(-1, 2)
+            packed.append((hh[:, 0], hh[:, 1], b.numpy().reshape(-1, 22)))
+        got = shard.unpack_paths(*shard.stage_rank0(packed, sizes))
+        q.put((got, shard.gather_ok(got, range(n_queries), sizes)))
     else:
-        dist.send(hdr, dst=0)
-        dist.send(body, dst=0)
+        dist.send(torch.from_numpy(np.stack([ids, rows], 1).reshape(-1).copy()), dst=0)
+        dist.send(torch.from_numpy(data.reshape(-1).copy()), dst=0)
     dist.barrier()
     dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3, 4, 5, 8])
+def test_gather_layout_and_staging(world):
+    """tcmp_gather_layout (rank 0's receive offsets, libtcmp.so) + shard.pack_paths /
+    stage_rank0 / unpack_paths at world sizes 2..8, ragged: ranks without queries, queries
+    without rows (failed plans), 64 C4 queries dealt round-robin."""
+    from torque_constrained_motion_planning_amd import _lib, shard
+    rng = np.random.default_rng(world)
+    n_q = 64
+    paths = {qid: rng.normal(size=(int(rng.integers(0, 40)) * (qid % 5 != 0), 22))
+             for qid in range(n_q)}
+    packed = []
+    for r in range(world):
+        mine = shard.queries_for_rank(n_q, world, r) if r != 1 else []  # rank 1 plans nothing
+        packed.append(shard.pack_paths([paths[i] for i in mine], mine))
+    sizes = np.array([[len(i), int(rw.sum())] for i, rw, _ in packed], dtype=np.int64)
+    q_off, r_off, tq, tr = _lib.gather_layout(sizes)
+    assert tq == sizes[:, 0].sum() and tr == sizes[:, 1].sum()
+    assert q_off[0] == 0 and r_off[0] == 0
+    assert np.array_equal(np.diff(q_off), sizes[:-1, 0]) and np.array_equal(np.diff(r_off), sizes[:-1, 1])
+    ids, rows, body = shard.stage_rank0(packed, sizes)
+    assert (ids >= 0).all() and not np.isnan(body).any()  # every slot written exactly
+    got = shard.unpack_paths(ids, rows, body)
+    expect = [i for r in range(world) if r != 1 for i in shard.queries_for_rank(n_q, world, r)]
+    assert shard.gather_ok(got, expect, sizes)
+    assert list(ids) == expect  # rank order, then each rank's own order
+    for qid in expect:
+        assert np.array_equal(got[qid], paths[qid])
+    # a lost or duplicated path fails the check
+    assert not shard.gather_ok({k: v for k, v in got.items() if k != expect[-1]}, expect, sizes)
+    assert not shard.gather_ok(got, expect + [999], sizes)
+    with pytest.raises(_lib.TcmpError):
+        _lib.gather_layout(-sizes - 1)
+
+
+def _rdzv_fail_worker(rank, world, port, job, q):
+    sys.path.insert(0, REPO)
+    os.environ["TCMP_JOB_ID"] = job
+    from torque_constrained_motion_planning_amd import _lib
+    try:
+        _lib.rendezvous(rank, world, "127.0.0.1", port, b"\1" * 16 if rank == 0 else bytes(16),
+                        timeout_ms=4000)
+        q.put((rank, "ok"))
+    except _lib.TcmpError as e:
+        q.put((rank, str(e)))
+
+
+@pytest.mark.parametrize("case", ["missing_rank", "other_job"])
+def test_rendezvous_fails_together(case):
+    """A rank that never arrives (world 3, two ranks started) or a rank of another job makes
+    every started rank fail within the timeout -- nobody receives the id and goes on alone."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    if case == "missing_rank":
+        specs = [(0, 3, "a"), (1, 3, "a")]
+    else:
+        specs = [(0, 2, "a"), (1, 2, "b")]
+    procs = [ctx.Process(target=_rdzv_fail_worker, args=(r, w, port, j, q)) for r, w, j in specs]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert all(v != "ok" for v in got.values()), got
 
 
 def test_round_robin_deal():
@@ -157,13 +228,14 @@ def test_gather_two_ranks_gloo():
     procs = [ctx.Process(target=_shard_worker, args=(r, 2, port, n_queries, q)) for r in range(2)]
     for p in procs:
         p.start()
-    got = q.get(timeout=240)
+    got, ok = q.get(timeout=240)
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle as O
     from torque_constrained_motion_planning_amd import shard
+    assert ok
     assert sorted(got) == list(range(n_queries))
     for qid in range(n_queries):
         ref = shard.pack_trajectory(_plan(O, qid))

@@ -1,0 +1,134 @@
+"""Body-level collision check of the grasp configuration (tcmp_check_body / tcmp_base_pd).
+
+The reference rejects a grasp configuration when any(pairwise_collision(robot, b) for b in
+obstacles) (franka_ik_fast.py:78, panda_primitives.py:260): body_collision ->
+get_closest_points(max_distance=-MAX_DISTANCE) over every link of the robot body
+(utils.py:2781,2833,2866-2880), so the static base panda_link0 counts too, at the same
+-0.04 penetration threshold as the moving links.  Parity: the oracle's brute-force
+hull-vs-hull depth of link0 (oracle/tcmp_oracle.c orc_base_pd / orc_body_collision).
+"""
+import random as pyrandom
+
+import numpy as np
+import pytest
+
+import oracle as O  # noqa: E402  (test infrastructure)
+
+pytestmark = pytest.mark.gpu
+
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+
+
+@pytest.fixture(scope="module")
+def eng():
+    from torque_constrained_motion_planning_amd import _lib
+    e = _lib.Engine(0)
+    yield e
+    e.close()
+
+
+def _box_behind_base(depth, half=0.05, z=0.05):
+    """A cube behind panda_link0 (-x side, away from the arm) whose depth into link0's hull
+    is `depth`, located by bisection on the oracle's depth."""
+    from torque_constrained_motion_planning_amd.scene import Box
+    lo, hi = -0.45, -0.12
+    for _ in range(60):
+        x = 0.5 * (lo + hi)
+        pd = O.base_pd(Box(center=(x, 0.0, z), size=(2 * half,) * 3).obb15()[None])[0]
+        if pd < depth:
+            lo = x
+        else:
+            hi = x
+    return Box(center=(0.5 * (lo + hi), 0.0, z), size=(2 * half,) * 3)
+
+
+def test_base_pd_vs_oracle(eng):
+    from torque_constrained_motion_planning_amd.scene import (Box, mesh_pack, obstacle_array,
+                                                               random_mesh_scene, rotation_rpy)
+    rng = np.random.default_rng(5)
+    boxes = [_box_behind_base(d) for d in (0.01, 0.03, 0.05, 0.06)]
+    for _ in range(60):
+        c = rng.uniform([-0.3, -0.3, -0.1], [0.3, 0.3, 0.3])
+        rot = rotation_rpy(*rng.uniform(-np.pi, np.pi, 3)) if rng.random() < 0.5 else None
+        boxes.append(Box(center=c, size=rng.uniform(0.02, 0.3, 3), rotation=rot))
+    obs = obstacle_array(boxes)
+    meshes = random_mesh_scene(rng, 24, lo=(-0.35, -0.35, -0.1), hi=(0.35, 0.35, 0.3))
+    pack = mesh_pack(meshes)
+    eng.set_scene(obs, pack)
+    got = eng.base_pd()
+    O.set_meshes(pack)
+    try:
+        ref = O.base_pd(obs)
+    finally:
+        O.set_meshes(None)
+    assert got.shape == ref.shape == (len(boxes) + 24,)
+    assert np.abs(got - ref).max() < 1e-9, np.abs(got - ref).max()
+    assert np.array_equal(got >= 0.04, ref >= 0.04)
+    hits = (ref >= 0.04).sum()
+    assert 0 < hits < len(ref)
+    # the bisected boxes sit at their depths
+    assert np.allclose(got[:4], [0.01, 0.03, 0.05, 0.06], atol=1e-9)
+
+
+def test_check_body_vs_oracle(eng):
+    from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene
+    rng = np.random.default_rng(8)
+    base_hit = _box_behind_base(0.05)
+    base_near = _box_behind_base(0.03)
+    q = LO + (HI - LO) * rng.random((400, 7))
+    q[::7] = np.clip(q[::7] * 1.2, -4, 4)  # some outside the limits: no limit test here
+    for extra, expect_all in (([base_hit], True), ([base_near], None), ([], None)):
+        obs = obstacle_array(random_box_scene(rng, 8) + extra)
+        eng.set_scene(obs)
+        got = eng.collides_body(q)
+        ref = np.array([O.body_collision(x, obs, cull=2) for x in q])
+        assert np.array_equal(got, ref)
+        if expect_all:
+            assert got.all()
+        else:
+            # moving links only, limits ignored: matches collision_fn on in-limit configs
+            inl = np.all((q >= LO) & (q <= HI), axis=1)
+            coll = eng.collides(q)
+            assert np.array_equal(got[inl], coll[inl])
+            assert not got[~inl].all()
+
+
+def _problem(extra):
+    from torque_constrained_motion_planning_amd.scene import Box, PandaRobot, Payload
+    from torque_constrained_motion_planning_amd.utils import Problem
+    table = Box(center=(0.5, 0.0, -0.02), size=(0.6, 1.0, 0.04))
+    return Problem(PandaRobot(), [table] + extra, Payload.coke(1.0), 1.0, 1.0, torque_test="rne")
+
+
+@pytest.mark.parametrize("depth,rejected", [(0.05, True), (0.03, False)])
+def test_grasp_rejected_by_link0(capsys, depth, rejected):
+    """A box into panda_link0 by 0.05 m (clear of every moving link) makes the grasp
+    configuration fail the body check -> 'Grasp IK failure', None; at 0.03 m it plans."""
+    from torque_constrained_motion_planning_amd import _lib
+    from torque_constrained_motion_planning_amd import ik as IK
+    from torque_constrained_motion_planning_amd import panda_primitives as PP
+    from torque_constrained_motion_planning_amd.scene import obstacle_array
+    box = _box_behind_base(depth)
+    problem = _problem([box])
+    start = IK.TOP_HOLDING_LEFT_ARM
+    pose = ((0.45, 0.1, 0.2), IK.quat_from_euler((0, 0, 0)))
+    # the box is clear of the moving links at the start and at the box-free grasp conf
+    free = _problem([])
+    np.random.seed(3)
+    pyrandom.seed(3)
+    g = IK.grasp_conf_for_pose(free, start, pose, engine=_lib.engine())
+    assert g is not None
+    obs = obstacle_array([box])
+    assert not O.collision(np.array(g), obs) and not O.collision(np.array(start), obs)
+    assert O.body_collision(np.array(g), obs) == rejected
+    capsys.readouterr()
+    np.random.seed(3)
+    pyrandom.seed(3)
+    traj = PP.planner_fn_force_aware(start, pose, problem)
+    out = capsys.readouterr().out
+    if rejected:
+        assert traj is None
+        assert "Grasp IK failure" in out and "found grasp" not in out
+    else:
+        assert "Grasp IK failure" not in out and "found grasp" in out

@@ -127,3 +127,56 @@ def test_c3_full_size_properties(eng):
             sel = np.arange(0, len(q), max(1, len(q) // 500))
             for i in sel:
                 assert O.torque_ok(q[i], 2, 5.0, qd=qd[i], qdd=qdd[i])
+
+
+def _digest(a):
+    import hashlib
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.mark.parametrize("name", ["c3", "c5"])
+def test_bench_query_vs_oracle_fixture(eng, name):
+    """The bench's own query at its own size, bit for bit against the oracle's batched
+    restatement (tests/golden/fullsize_<name>.npz, made by tests/golden/gen_fullsize.py):
+    C3 = bench.py make_query(1234), 16 boxes, 5 kg, rne, 1e6 samples, B = 262,144, seed 1234
+    (step 0 of rank 0); C5 = make_query(1234, n_mesh=256), 2e5 samples.  The scene is
+    regenerated on the device by bench.make_query and must be the fixture's; then the final
+    tree (configs, costs, parents: sha256), counters, waypoints and trajectory rows match."""
+    import os
+    import sys
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden",
+                        "fullsize_%s.npz" % name)
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated")
+    F = np.load(path)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n_mesh = int(F["n_mesh"])
+    obs, pack, goal = bench.make_query(1234, n_obs=16 if not n_mesh else 0, mode=2, mass=5.0,
+                                       engine=eng, n_mesh=n_mesh)
+    assert np.array_equal(obs, F["obs"]) and np.array_equal(goal, F["goal"])
+    if n_mesh:
+        import hashlib
+        h = hashlib.sha256()
+        for f in ("verts", "vert_off", "planes", "plane_off", "edges", "edge_off", "boxes"):
+            h.update(np.ascontiguousarray(getattr(pack, f)).tobytes())
+        assert h.hexdigest() == str(F["sha_pack"])
+    r, out = bench.run_query(eng, obs, goal, int(F["samples"]), int(F["batch"]), int(F["seed"]),
+                             meshes=pack)
+    assert (r.n_samples, r.n_nodes, r.edge_steps, r.goal_node, r.status) == \
+        (int(F["n_samples"]), int(F["n_nodes"]), int(F["edge_steps"]), int(F["goal_node"]),
+         int(F["status"]))
+    cfg, cost, par, n = eng.plan_tree(r.n_nodes)
+    stride = F["tree_stride"]
+    assert np.array_equal(cfg[stride], F["tree_cfg_sel"])
+    assert np.array_equal(par[stride], F["tree_parent_sel"])
+    assert _digest(cfg) == str(F["sha_cfg"])
+    assert _digest(cost) == str(F["sha_cost"])
+    assert _digest(par.astype(np.int32)) == str(F["sha_parent"])
+    if int(F["status"]) in (0, 3):
+        assert (r.n_waypoints, r.n_traj) == (int(F["n_waypoints"]), int(F["n_traj"]))
+        assert np.array_equal(out["waypoints"], F["waypoints"])
+        sel = F["traj_sel"]
+        for k in ("q", "qd", "qdd"):
+            assert np.abs(out[k][sel] - F[k]).max() < 1e-9, k
+        assert np.abs(out["psg"][sel] - F["psg"]).max() < 1e-12

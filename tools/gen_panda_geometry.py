@@ -24,6 +24,12 @@ Per link we store, in the link frame:
   * hull edge directions     (edge x box-axis SAT candidates)
   * outer OBB  (hull subset)  -> conservative "free" cull
   * inner box  (subset hull)  -> conservative "collision" accept
+
+The static base panda_link0 (panda_mod.urdf:7-11, link0.stl, no collision origin) is not a
+moving link, but the body-level check of a grasp configuration (pairwise_collision(robot, b),
+franka_ik_fast.py:78, panda_primitives.py:260) covers every link of the robot body.  Its
+hull goes to panda_base.inc (world frame = base frame) with the same vertex / facet / edge
+layout.
 """
 import os
 import struct
@@ -38,6 +44,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 OUT_INC = os.path.join(REPO, "torque_constrained_motion_planning_amd", "csrc", "panda_geometry.inc")
 OUT_NPZ = os.path.join(REPO, "torque_constrained_motion_planning_amd", "data", "panda_geometry.npz")
+OUT_BASE = os.path.join(REPO, "torque_constrained_motion_planning_amd", "csrc", "panda_base.inc")
 
 LINKS = ["link1", "link2", "link3", "link4", "link5", "link6", "link7", "hand",
          "finger", "finger"]
@@ -224,6 +231,39 @@ def main():
     os.makedirs(os.path.dirname(OUT_INC), exist_ok=True)
     with open(OUT_INC, "w") as f:
         f.write("\n".join(L) + "\n")
+    base = link_data("link0", flip_z_pi=False)
+    print("panda_link0 verts", len(base["verts"]), "planes", len(base["planes"]), "edges",
+          len(base["edges"]), file=sys.stderr)
+    B = []
+    B.append("/* GENERATED by tools/gen_panda_geometry.py -- do not edit.")
+    B.append(" * Static base panda_link0 (panda_mod.urdf:7-11, link0.stl): convex hull in the base")
+    B.append(" * (= world) frame for the body-level grasp check.  Data only. */")
+    B.append("#ifndef TCMP_GEO_QUAL")
+    B.append("#define TCMP_GEO_QUAL static const")
+    B.append("#endif")
+    B.append("#define TCMP_BASE_NV %d" % len(base["verts"]))
+    B.append("#define TCMP_BASE_NF %d" % len(base["planes"]))
+    B.append("#define TCMP_BASE_NE %d" % len(base["edges"]))
+    B.append("/* verts: x y z 0 */")
+    B.append("TCMP_GEO_QUAL double tcmp_base_verts[TCMP_BASE_NV * 4] = {")
+    for p in base["verts"]:
+        B.append("  %s, %s, %s, 0.0," % tuple(fmt(x) for x in p))
+    B.append("};")
+    B.append("/* planes: nx ny nz dmax */")
+    B.append("TCMP_GEO_QUAL double tcmp_base_planes[TCMP_BASE_NF * 4] = {")
+    for p in base["planes"]:
+        B.append("  %s, %s, %s, %s," % tuple(fmt(x) for x in p[:4]))
+    B.append("};")
+    B.append("/* edges: va vb f1 f2 (rows of the arrays above) */")
+    B.append("TCMP_GEO_QUAL int tcmp_base_edges[TCMP_BASE_NE * 4] = {")
+    for a, b, f1, f2 in base["edge_idx"]:
+        B.append("  %d, %d, %d, %d," % (a, b, f1, f2))
+    B.append("};")
+    lo, hi = base["verts"].min(0), base["verts"].max(0)
+    B.append("/* AABB lo(3) hi(3) */")
+    B.append("TCMP_GEO_QUAL double tcmp_base_aabb[6] = {%s};" % ", ".join(fmt(x) for x in list(lo) + list(hi)))
+    with open(OUT_BASE, "w") as f:
+        f.write("\n".join(B) + "\n")
     os.makedirs(os.path.dirname(OUT_NPZ), exist_ok=True)
     np.savez(OUT_NPZ,
              verts=np.concatenate([d["verts"] for d in links]),
@@ -234,7 +274,9 @@ def main():
              vert_off=ov, plane_off=of, edge_off=oe,
              boxes=np.array([np.concatenate([d["obb_c"], d["obb_R"].reshape(-1), d["obb_half"],
                                              d["in_half"]]) for d in links]),
-             link_names=np.array(LINK_NAMES))
+             link_names=np.array(LINK_NAMES),
+             base_verts=base["verts"], base_planes=base["planes"][:, :4],
+             base_edge_idx=base["edge_idx"])
     print("wrote", OUT_INC, OUT_NPZ, file=sys.stderr)
 
 

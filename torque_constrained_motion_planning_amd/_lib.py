@@ -25,6 +25,7 @@ EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
     "tcmp_synchronize",
     "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_check_body", "tcmp_base_pd",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_run_shared", "tcmp_plan_run_group",
@@ -32,6 +33,7 @@ EXPORTS = [
     "tcmp_debug_counters",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
     "tcmp_dist_barrier", "tcmp_dist_allreduce", "tcmp_dist_allgather_i64", "tcmp_gather_paths",
+    "tcmp_gather_layout", "tcmp_dist_rccl_ranks",
 ]
 TRAJ_COLS = 22
 REDUCE_SUM, REDUCE_MAX = 0, 1
@@ -108,6 +110,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
                                      ctypes.c_double, _i32p]
         L.tcmp_check_configs.argtypes = [vp, _dp, ctypes.c_int64, _i32p]
+        L.tcmp_check_body.argtypes = [vp, _dp, ctypes.c_int64, _i32p]
+        L.tcmp_base_pd.argtypes = [vp, _dp, ctypes.c_int32]
         L.tcmp_check_edges.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, ctypes.c_int32,
                                        ctypes.c_double, _i32p, _i32p, _dp]
         L.tcmp_nearest.argtypes = [vp, _dp, ctypes.c_int64, _dp, ctypes.c_int64, _dp, _i32p]
@@ -136,8 +140,10 @@ def load_library(path=LIB_PATH):
         L.tcmp_dist_barrier.argtypes = [vp]
         L.tcmp_dist_allreduce.argtypes = [vp, _dp, i32, i32]
         L.tcmp_dist_allgather_i64.argtypes = [vp, _i64p, i32, _i64p]
-        L.tcmp_gather_paths.argtypes = [vp, i32, _i64p, _i64p, _dp, ctypes.c_int64,
+        L.tcmp_gather_paths.argtypes = [vp, i32, _i64p, _i64p, _dp, _i64p, ctypes.c_int64,
                                         ctypes.c_int64, _i64p, _i64p, _dp, _i64p, _i64p]
+        L.tcmp_gather_layout.argtypes = [i32, _i64p, _i64p, _i64p, _i64p, _i64p]
+        L.tcmp_dist_rccl_ranks.argtypes = [vp, _i32p]
         _lib = L
         return L
 
@@ -234,6 +240,7 @@ class Engine:
                                                       int(len(meshes))))
         self._mesh_key = mkey
         self._scene_key = key
+        self._n_scene = len(obb) + (len(meshes) if meshes is not None else 0)
 
     # ---- batched physics --------------------------------------------------------------
     def rne(self, q, qd, qdd, payload_mass=0.0):
@@ -289,6 +296,21 @@ class Engine:
         out = np.zeros(len(q), dtype=np.int32)
         self._check(self.L.tcmp_check_configs(self.h, _d(q), len(q), out.ctypes.data_as(_i32p)))
         return out.astype(bool)
+
+    def collides_body(self, q):
+        """any(pairwise_collision(robot, b) for b in obstacles) per configuration: every robot
+        link, the static base panda_link0 included, no joint-limit test (tcmp_check_body)."""
+        q = _rows(q, "q")
+        out = np.zeros(len(q), dtype=np.int32)
+        self._check(self.L.tcmp_check_body(self.h, _d(q), len(q), out.ctypes.data_as(_i32p)))
+        return out.astype(bool)
+
+    def base_pd(self):
+        """panda_link0's penetration depth against each box, then each mesh (tcmp_base_pd)."""
+        n = getattr(self, "_n_scene", 0)
+        out = np.zeros(n)
+        self._check(self.L.tcmp_base_pd(self.h, _d(out) if n else None, n))
+        return out
 
     def check_edges(self, q_from, q_to, mode, mass, resolutions=None):
         a = _rows(q_from, "from"); b = _rows(q_to, "to")
@@ -440,17 +462,28 @@ class Comm:
                                              out.ctypes.data_as(_i64p)))
         return out.reshape(self.world, len(v))
 
-    def gather_paths(self, ids, rows, data, cap_queries, cap_rows):
-        """tcmp_gather_paths: (ids, rows, data) on rank 0, None elsewhere."""
+    def rccl_ranks(self):
+        """ncclCommCount of the communicator (0: a one-rank job, no RCCL communicator)."""
+        n = ctypes.c_int32(0)
+        check(self.L.tcmp_dist_rccl_ranks(self.h, ctypes.byref(n)))
+        return n.value
+
+    def gather_paths(self, ids, rows, data, cap_queries, cap_rows, sizes=None):
+        """tcmp_gather_paths: (ids, rows, data) on rank 0, None elsewhere.  sizes: the
+        (world, 2) all-gathered (queries, rows) when the caller has them (no second
+        size exchange)."""
         ids = np.ascontiguousarray(ids, dtype=np.int64)
         rows = np.ascontiguousarray(rows, dtype=np.int64)
         data = np.ascontiguousarray(data, dtype=np.float64).reshape(-1, TRAJ_COLS)
+        sz = None if sizes is None else np.ascontiguousarray(sizes, dtype=np.int64).reshape(-1)
         oi = np.zeros(max(cap_queries, 1), dtype=np.int64)
         orows = np.zeros(max(cap_queries, 1), dtype=np.int64)
         od = np.zeros((max(cap_rows, 1), TRAJ_COLS))
         nq, nr = ctypes.c_int64(0), ctypes.c_int64(0)
         check(self.L.tcmp_gather_paths(self.h, len(ids), ids.ctypes.data_as(_i64p),
-                                       rows.ctypes.data_as(_i64p), _d(data), int(cap_queries),
+                                       rows.ctypes.data_as(_i64p), _d(data),
+                                       None if sz is None else sz.ctypes.data_as(_i64p),
+                                       int(cap_queries),
                                        int(cap_rows), oi.ctypes.data_as(_i64p),
                                        orows.ctypes.data_as(_i64p), _d(od), ctypes.byref(nq),
                                        ctypes.byref(nr)))
@@ -468,6 +501,19 @@ class Comm:
             self.close()
         except Exception:
             pass
+
+
+def gather_layout(sizes):
+    """tcmp_gather_layout: (q_off, r_off, total_q, total_r) of rank 0's receive buffer from
+    the (world, 2) per-rank (queries, rows)."""
+    sz = np.ascontiguousarray(np.asarray(sizes, dtype=np.int64).reshape(-1, 2))
+    w = len(sz)
+    qo = np.zeros(w, dtype=np.int64); ro = np.zeros(w, dtype=np.int64)
+    tq, tr = ctypes.c_int64(0), ctypes.c_int64(0)
+    check(load_library().tcmp_gather_layout(w, sz.ctypes.data_as(_i64p), qo.ctypes.data_as(_i64p),
+                                            ro.ctypes.data_as(_i64p), ctypes.byref(tq),
+                                            ctypes.byref(tr)))
+    return qo, ro, tq.value, tr.value
 
 
 def rendezvous(rank, world, addr, port, blob, timeout_ms=60000):

@@ -23,6 +23,7 @@
 #include <unistd.h>
 
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <thread>
@@ -81,8 +82,21 @@ bool recv_all(int fd, void* p, size_t n, int timeout_ms) {
 
 struct Hello {
   uint64_t magic;
+  uint64_t job;  // job identity: a stale or concurrent job on the same port is turned away
   int32_t rank, world, nbytes, pad;
 };
+
+// FNV-1a of the launcher's run id (TCMP_JOB_ID, else TORCHELASTIC_RUN_ID) and the world size
+uint64_t job_nonce(int world, int port) {
+  const char* id = std::getenv("TCMP_JOB_ID");
+  if (!id || !*id) id = std::getenv("TORCHELASTIC_RUN_ID");
+  uint64_t x = 1469598103934665603ull;
+  auto mix = [&](unsigned char b) { x = (x ^ b) * 1099511628211ull; };
+  for (const char* p = id ? id : ""; *p; ++p) mix((unsigned char)*p);
+  for (int k = 0; k < 4; ++k) mix((unsigned char)(world >> (8 * k)));
+  for (int k = 0; k < 4; ++k) mix((unsigned char)(port >> (8 * k)));
+  return x;
+}
 
 }  // namespace
 
@@ -109,29 +123,29 @@ int rank(const tcmp_comm* c) { return c->rank; }
 int world(const tcmp_comm* c) { return c->world; }
 int device(const tcmp_comm* c) { return c->device; }
 
-int allreduce_min_i64(tcmp_comm* c, int64_t* d, int n, hipStream_t s) {
-  if (c->world == 1 || n <= 0) return 0;
-  NCCLD(ncclAllReduce(d, d, (size_t)n, ncclInt64, ncclMin, c->nccl, s));
+int RcclExchange::min_i64(int64_t* d, int n, hipStream_t s) {
+  if (c_->world == 1 || n <= 0) return 0;
+  NCCLD(ncclAllReduce(d, d, (size_t)n, ncclInt64, ncclMin, c_->nccl, s));
   return 0;
 }
 
-int allgather_i64(tcmp_comm* c, const int64_t* send, int64_t* recv, int n, hipStream_t s) {
+int RcclExchange::allgather_i64(const int64_t* send, int64_t* recv, int n, hipStream_t s) {
   if (n <= 0) return 0;
-  if (c->world == 1) {
+  if (c_->world == 1) {
     HIPD(hipMemcpyAsync(recv, send, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToDevice, s));
     return 0;
   }
-  NCCLD(ncclAllGather(send, recv, (size_t)n, ncclInt64, c->nccl, s));
+  NCCLD(ncclAllGather(send, recv, (size_t)n, ncclInt64, c_->nccl, s));
   return 0;
 }
 
-int bcast_group(tcmp_comm* c, const Bcast* ops, int n_ops, hipStream_t s) {
-  if (c->world == 1 || n_ops <= 0) return 0;
+int RcclExchange::bcast(const Bcast* ops, int n_ops, hipStream_t s) {
+  if (c_->world == 1 || n_ops <= 0) return 0;
   NCCLD(ncclGroupStart());
   for (int i = 0; i < n_ops; ++i) {
     if (ops[i].bytes == 0) continue;
     const ncclResult_t r = ncclBroadcast(ops[i].ptr, ops[i].ptr, ops[i].bytes, ncclUint8,
-                                         ops[i].root, c->nccl, s);
+                                         ops[i].root, c_->nccl, s);
     if (r != ncclSuccess) {
       (void)ncclGroupEnd();
       return fail(-5, std::string("ncclBroadcast: ") + ncclGetErrorString(r));
@@ -139,6 +153,19 @@ int bcast_group(tcmp_comm* c, const Bcast* ops, int n_ops, hipStream_t s) {
   }
   NCCLD(ncclGroupEnd());
   return 0;
+}
+
+void gather_layout(int world, const int64_t* sizes, int64_t* q_off, int64_t* r_off,
+                   int64_t* total_q, int64_t* total_r) {
+  int64_t q = 0, r = 0;
+  for (int k = 0; k < world; ++k) {
+    if (q_off) q_off[k] = q;
+    if (r_off) r_off[k] = r;
+    q += sizes[2 * k];
+    r += sizes[2 * k + 1];
+  }
+  if (total_q) *total_q = q;
+  if (total_r) *total_r = r;
 }
 
 }  // namespace tcmp_dist
@@ -161,6 +188,7 @@ int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port,
   sockaddr_in sa;
   std::memcpy(&sa, res->ai_addr, sizeof(sa));
   ::freeaddrinfo(res);
+  const uint64_t job = job_nonce(world, port);
   if (rank == 0) {
     const int ls = ::socket(AF_INET, SOCK_STREAM, 0);
     if (ls < 0) return fail(-1, "tcmp_rendezvous: socket");
@@ -170,7 +198,8 @@ int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port,
       ::close(ls);
       return fail(-1, "tcmp_rendezvous: cannot listen on " + std::string(addr) + ":" + ps);
     }
-    std::vector<int> seen(world, 0);
+    // phase 1: every other rank introduces itself; the connections stay open
+    std::vector<int> fds(world, -1);
     int got = 0, rc = 0;
     while (got < world - 1) {
       const int left = (int)std::chrono::duration_cast<std::chrono::milliseconds>(
@@ -184,17 +213,26 @@ int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port,
       const int fd = ::accept(ls, nullptr, nullptr);
       if (fd < 0) continue;
       Hello h{};
-      if (recv_all(fd, &h, sizeof(h), 5000) && h.magic == kMagic && h.world == world &&
-          h.nbytes == nbytes && h.rank > 0 && h.rank < world && !seen[h.rank]) {
-        Hello ack{kMagic, 0, world, nbytes, 0};
-        if (send_all(fd, &ack, sizeof(ack)) && send_all(fd, blob, (size_t)nbytes)) {
-          seen[h.rank] = 1;
-          ++got;
-        }
+      if (recv_all(fd, &h, sizeof(h), 5000) && h.magic == kMagic && h.job == job &&
+          h.world == world && h.nbytes == nbytes && h.rank > 0 && h.rank < world &&
+          fds[h.rank] < 0) {
+        fds[h.rank] = fd;
+        ++got;
+      } else {
+        ::close(fd);  // a stranger, a stale job, or a duplicate rank
       }
-      ::close(fd);
     }
     ::close(ls);
+    // phase 2: the blob goes out only once the whole world has arrived; on a timeout every
+    // connection closes unanswered, so every waiting rank fails instead of one part of the
+    // job entering the communicator set-up without the others
+    for (int r = 1; r < world && !rc; ++r) {
+      Hello ack{kMagic, job, 0, world, nbytes, 0};
+      if (!send_all(fds[r], &ack, sizeof(ack)) || !send_all(fds[r], blob, (size_t)nbytes))
+        rc = fail(-1, "tcmp_rendezvous: lost rank " + std::to_string(r));
+    }
+    for (int fd : fds)
+      if (fd >= 0) ::close(fd);
     return rc;
   }
   // other ranks: connect (rank 0 may not be listening yet), introduce, receive the blob
@@ -202,10 +240,10 @@ int tcmp_rendezvous(int32_t rank, int32_t world, const char* addr, int32_t port,
     const int fd = ::socket(AF_INET, SOCK_STREAM, 0);
     if (fd < 0) return fail(-1, "tcmp_rendezvous: socket");
     if (::connect(fd, reinterpret_cast<sockaddr*>(&sa), sizeof(sa)) == 0) {
-      Hello h{kMagic, rank, world, nbytes, 0}, ack{};
+      Hello h{kMagic, job, rank, world, nbytes, 0}, ack{};
       const bool ok = send_all(fd, &h, sizeof(h)) && recv_all(fd, &ack, sizeof(ack), timeout_ms) &&
-                      ack.magic == kMagic && ack.world == world && ack.nbytes == nbytes &&
-                      recv_all(fd, blob, (size_t)nbytes, timeout_ms);
+                      ack.magic == kMagic && ack.job == job && ack.world == world &&
+                      ack.nbytes == nbytes && recv_all(fd, blob, (size_t)nbytes, timeout_ms);
       ::close(fd);
       if (ok) return 0;
       return fail(-1, "tcmp_rendezvous: handshake with rank 0 failed");
@@ -308,9 +346,19 @@ int tcmp_dist_allgather_i64(tcmp_comm* c, const int64_t* in, int32_t n, int64_t*
   return 0;
 }
 
+int tcmp_gather_layout(int32_t world, const int64_t* sizes, int64_t* q_off, int64_t* r_off,
+                       int64_t* total_q, int64_t* total_r) {
+  if (world < 1 || !sizes) return fail(-1, "bad arguments");
+  for (int k = 0; k < 2 * world; ++k)
+    if (sizes[k] < 0) return fail(-1, "negative size");
+  tcmp_dist::gather_layout(world, sizes, q_off, r_off, total_q, total_r);
+  return 0;
+}
+
 int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const int64_t* rows,
-                      const double* data, int64_t cap_queries, int64_t cap_rows, int64_t* out_ids,
-                      int64_t* out_rows, double* out_data, int64_t* n_queries, int64_t* n_rows) {
+                      const double* data, const int64_t* sizes_in, int64_t cap_queries,
+                      int64_t cap_rows, int64_t* out_ids, int64_t* out_rows, double* out_data,
+                      int64_t* n_queries, int64_t* n_rows) {
   if (!c || n_local < 0 || (n_local > 0 && (!ids || !rows)) || !n_queries || !n_rows)
     return fail(-1, "bad arguments");
   int64_t my_rows = 0;
@@ -319,35 +367,34 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
     my_rows += rows[i];
   }
   if (my_rows > 0 && !data) return fail(-1, "null trajectory rows");
-  // 1. sizes of every rank's contribution
+  // 1. sizes of every rank's contribution (unless the caller already all-gathered them)
   const int W = c->world;
   std::vector<int64_t> sizes(2 * (size_t)W);
-  const int64_t mine[2] = {n_local, my_rows};
-  if (int rc = tcmp_dist_allgather_i64(c, mine, 2, sizes.data())) return rc;
-  int64_t tq = 0, tr = 0;
-  for (int r = 0; r < W; ++r) {
-    tq += sizes[2 * r];
-    tr += sizes[2 * r + 1];
-  }
-  if (c->rank == 0) {
-    *n_queries = tq;
-    *n_rows = tr;
+  if (sizes_in) {
+    std::memcpy(sizes.data(), sizes_in, sizes.size() * sizeof(int64_t));
+    if (sizes[2 * c->rank] != n_local || sizes[2 * c->rank + 1] != my_rows)
+      return fail(-1, "sizes[rank] does not match this rank's paths");
   } else {
-    *n_queries = 0;
-    *n_rows = 0;
+    const int64_t mine[2] = {n_local, my_rows};
+    if (int rc = tcmp_dist_allgather_i64(c, mine, 2, sizes.data())) return rc;
   }
+  // 2. rank 0's receive layout: each rank's header / body rows in rank order
+  std::vector<int64_t> q_off((size_t)W), r_off((size_t)W);
+  int64_t tq = 0, tr = 0;
+  tcmp_dist::gather_layout(W, sizes.data(), q_off.data(), r_off.data(), &tq, &tr);
+  *n_queries = c->rank == 0 ? tq : 0;
+  *n_rows = c->rank == 0 ? tr : 0;
   std::vector<int64_t> hdr(2 * (size_t)n_local);
   for (int i = 0; i < n_local; ++i) {
     hdr[2 * i] = ids[i];
     hdr[2 * i + 1] = rows[i];
   }
-  // rank 0 only: every rank's header then every rank's body, in rank order
   std::vector<int64_t> all_hdr;
   std::vector<double> all_body;
   if (W > 1) {
     HIPD(hipSetDevice(c->device));
-    // device layout on rank 0: headers of all ranks, then bodies of all ranks; elsewhere the
-    // rank's own header and body
+    // device staging on rank 0: headers of all ranks, then bodies of all ranks; elsewhere
+    // the rank's own header and body
     const size_t hb = (size_t)(c->rank == 0 ? tq : n_local) * 2 * sizeof(int64_t);
     const size_t bb = (size_t)(c->rank == 0 ? tr : my_rows) * kCols * sizeof(double);
     const size_t hpad = (hb + 255) & ~size_t(255);
@@ -362,22 +409,24 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
       HIPD(hipMemcpyAsync(db, data, (size_t)my_rows * kCols * sizeof(double),
                           hipMemcpyHostToDevice, c->stream));
     NCCLD(ncclGroupStart());
+    ncclResult_t r = ncclSuccess;
     if (c->rank == 0) {
-      int64_t qo = sizes[0], ro = sizes[1];
-      for (int r = 1; r < W; ++r) {
-        const int64_t nq = sizes[2 * r], nr = sizes[2 * r + 1];
-        if (nq) NCCLD(ncclRecv(dh + 2 * qo, (size_t)(2 * nq), ncclInt64, r, c->nccl, c->stream));
-        if (nr) NCCLD(ncclRecv(db + kCols * ro, (size_t)(kCols * nr), ncclFloat64, r, c->nccl,
-                               c->stream));
-        qo += nq;
-        ro += nr;
+      for (int k = 1; k < W && r == ncclSuccess; ++k) {
+        const int64_t nq = sizes[2 * k], nr = sizes[2 * k + 1];
+        if (nq) r = ncclRecv(dh + 2 * q_off[k], (size_t)(2 * nq), ncclInt64, k, c->nccl, c->stream);
+        if (nr && r == ncclSuccess)
+          r = ncclRecv(db + kCols * r_off[k], (size_t)(kCols * nr), ncclFloat64, k, c->nccl,
+                       c->stream);
       }
     } else {
-      if (n_local) NCCLD(ncclSend(dh, (size_t)(2 * n_local), ncclInt64, 0, c->nccl, c->stream));
-      if (my_rows) NCCLD(ncclSend(db, (size_t)(kCols * my_rows), ncclFloat64, 0, c->nccl,
-                                  c->stream));
+      if (n_local) r = ncclSend(dh, (size_t)(2 * n_local), ncclInt64, 0, c->nccl, c->stream);
+      if (my_rows && r == ncclSuccess)
+        r = ncclSend(db, (size_t)(kCols * my_rows), ncclFloat64, 0, c->nccl, c->stream);
     }
-    NCCLD(ncclGroupEnd());
+    // the group is closed on every path, so later RCCL calls on this thread still work
+    const ncclResult_t re = ncclGroupEnd();
+    if (r != ncclSuccess) return fail(-5, std::string("ncclSend/ncclRecv: ") + ncclGetErrorString(r));
+    if (re != ncclSuccess) return fail(-5, std::string("ncclGroupEnd: ") + ncclGetErrorString(re));
     if (c->rank == 0) {
       all_hdr.resize(2 * (size_t)tq);
       all_body.resize((size_t)tr * kCols);
@@ -401,6 +450,16 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
     out_rows[i] = all_hdr[2 * i + 1];
   }
   if (tr) std::memcpy(out_data, all_body.data(), all_body.size() * sizeof(double));
+  return 0;
+}
+
+int tcmp_dist_rccl_ranks(const tcmp_comm* c, int32_t* n) {
+  if (!c || !n) return fail(-1, "bad arguments");
+  *n = 0;
+  if (!c->nccl) return 0;  // a one-rank job has no communicator
+  int k = 0;
+  NCCLD(ncclCommCount(c->nccl, &k));
+  *n = k;
   return 0;
 }
 

@@ -22,6 +22,9 @@
 #include <algorithm>
 #include <climits>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -328,6 +331,7 @@ __global__ __launch_bounds__(256) void k_cs_scatter(const int* bin, int n, int n
 #include "tcmp_nn32.h"
 #include "tcmp_insert.h"
 #include "tcmp_ik.h"
+#include "tcmp_base.h"
 
 // ------------------------------------------------------------------------------------------
 // k_edges: safe_path_force_aware(extend(from, to)) for n edges (rrt_star.py:90-98).
@@ -805,9 +809,10 @@ __global__ void k_traj_post(DevState* st) {
 // ------------------------------------------------------------------------------------------
 // utility kernels behind the batched C-ABI entry points
 // ------------------------------------------------------------------------------------------
+// collision_fn (limits, then every moving link); no_limits: the links only (body-level check)
 template <bool MESH>
 __global__ __launch_bounds__(256) void k_check_configs(const double* q, long long n, Scene sc_g,
-                                                       Geo g_g, int* collides) {
+                                                       Geo g_g, int* collides, int no_limits) {
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
@@ -820,7 +825,7 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
   double cq[7], sq[7];
   for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
   StepStats ss = {0, 0, 0};
-  const bool lim = act && limits_violated(x);
+  const bool lim = act && !no_limits && limits_violated(x);
   const bool c = collides_wave<MESH>(cq, sq, act && !lim, sc, g, ss) || lim;
   if (act) collides[i] = c ? 1 : 0;
 }
@@ -951,6 +956,8 @@ struct tcmp_handle {
   DBuf<int> mrange;
   std::vector<int> mrange_h;
   DBuf<double> mib, mv64, mp64, me64;
+  DBuf<double> base_geo;  // panda_link0 hull (tcmp_base.h), uploaded on first use
+  DBuf<double> base_pd;
   DBuf<float> mv32, mp32, me32;
   DBuf<float> lv32[2], lp32[2], le32[2];      // mesh LOD hulls (inner, outer), world frame
   // host copies of the user meshes' LOD hulls (tcmp_set_mesh_lods; cleared by tcmp_set_meshes)
@@ -1549,7 +1556,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->geo_ev.release();
   h->obs32.release();
   h->mrange.release();
-  for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64}) b->release();
+  for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64, &h->base_geo, &h->base_pd}) b->release();
   for (auto* b : {&h->mv32, &h->mp32, &h->me32}) b->release();
   for (int i = 0; i < 2; ++i) {
     for (auto* b : {&h->lv32[i], &h->lp32[i], &h->le32[i], &h->lodv3[i], &h->lodpl[i], &h->lodev[i]})
@@ -2034,8 +2041,74 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
   hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>, dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
-                     (long long)n, h->scene(), h->geo(), h->i0.p);
+                     (long long)n, h->scene(), h->geo(), h->i0.p, 0);
   HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+// panda_link0 against every obstacle of the scene (boxes, then user meshes) into h->base_pd
+static int launch_base_pd(tcmp_handle* h) {
+  const int nb = h->n_box + h->n_mesh;
+  if (nb == 0) return 0;
+  if (!h->base_geo.p) {
+    std::vector<double> g((size_t)4 * (TCMP_BASE_NV + TCMP_BASE_NF + TCMP_BASE_NE), 0.0);
+    double* gv = g.data();
+    double* gn = gv + 4 * TCMP_BASE_NV;
+    double* ge = gn + 4 * TCMP_BASE_NF;
+    for (int i = 0; i < 4 * TCMP_BASE_NV; ++i) gv[i] = tcmp_base_verts[i];
+    for (int i = 0; i < 4 * TCMP_BASE_NF; ++i) gn[i] = tcmp_base_planes[i];
+    for (int i = 0; i < TCMP_BASE_NE; ++i) {
+      const double* a = tcmp_base_verts + 4 * tcmp_base_edges[4 * i];
+      const double* b = tcmp_base_verts + 4 * tcmp_base_edges[4 * i + 1];
+      double e[3] = {b[0] - a[0], b[1] - a[1], b[2] - a[2]};
+      const double l = sqrt(e[0] * e[0] + e[1] * e[1] + e[2] * e[2]);
+      for (int k = 0; k < 3; ++k) ge[4 * i + k] = e[k] / l;
+    }
+    if (int rc = h->base_geo.ensure(g.size())) return rc;
+    HIPCHK(hipMemcpy(h->base_geo.p, g.data(), g.size() * sizeof(double), hipMemcpyHostToDevice));
+  }
+  if (int rc = h->base_pd.ensure((size_t)nb)) return rc;
+  const double4* b4 = reinterpret_cast<const double4*>(h->base_geo.p);
+  BaseGeo bg{b4, b4 + TCMP_BASE_NV, b4 + TCMP_BASE_NV + TCMP_BASE_NF};
+  hipLaunchKernelGGL(k_base_pd, dim3(nb), dim3(kBaseThreads), 0, h->stream, h->scene(), bg,
+                     h->n_box, h->base_pd.p);
+  HIPCHK(hipGetLastError());
+  return 0;
+}
+
+int tcmp_base_pd(tcmp_handle* h, double* pd, int32_t n) {
+  if (int rc = set_dev(h)) return rc;
+  if (n != h->n_box + h->n_mesh) return fail(-1, "n must be the scene's boxes + meshes");
+  if (n == 0) return 0;
+  if (!pd) return fail(-1, "bad arguments");
+  if (int rc = launch_base_pd(h)) return rc;
+  HIPCHK(hipMemcpyAsync(pd, h->base_pd.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
+                        h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collides) {
+  if (int rc = set_dev(h)) return rc;
+  if (n < 0 || (n > 0 && (!q || !collides))) return fail(-1, "bad arguments");
+  if (n == 0) return 0;
+  int rc = upload7(h, h->s0, q, n);
+  rc = rc ? rc : h->i0.ensure((size_t)n);
+  rc = rc ? rc : launch_base_pd(h);
+  if (rc) return rc;
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
+                     dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
+                     (long long)n, h->scene(), h->geo(), h->i0.p, 1);
+  HIPCHK(hipGetLastError());
+  const int nb = h->n_box + h->n_mesh;
+  if (nb) {
+    hipLaunchKernelGGL(k_body_merge, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->i0.p,
+                       (long long)n, h->base_pd.p, nb);
+    HIPCHK(hipGetLastError());
+  }
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                         h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -2264,7 +2337,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   HIPCHK(hipMemcpyAsync(h->s0.p, pn.sg, sizeof(pn.sg), hipMemcpyHostToDevice, h->stream));
   hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
                      dim3(1), dim3(256), lds_bytes(h), h->stream, h->s0.p, 2LL, h->scene(),
-                     h->geo(), h->i0.p);
+                     h->geo(), h->i0.p, 0);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(pn.coll, h->i0.p, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   // root node (OptimalNode(start), rrt_star.py:155)
@@ -2514,16 +2587,17 @@ int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goa
   return 0;
 }
 
-int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_t batch) {
-  if (int rc = set_dev(h)) return rc;
-  if (!c) return fail(-1, "null comm");
-  const int W = tcmp_dist::world(c), r = tcmp_dist::rank(c);
-  if (W == 1) return tcmp_plan_run(h, n_samples, batch);
-  if (int rc = sr_check(h, n_samples, batch, W)) return rc;
+// The rounds of one engine in a shared tree, over any transport (tcmp_dist_internal.h): the
+// RCCL communicator of tcmp_plan_run_shared and the host-thread group of tcmp_plan_run_group
+// run this same loop, so the group tests on one GPU cover the multi-GPU round logic.
+static int shared_rounds(tcmp_handle* h, tcmp_dist::RoundExchange& X, long long n_samples,
+                         int batch) {
+  const int W = X.world(), r = X.rank();
   long long T = 0;
   if (int rc = sr_tree_size(h, &T)) return rc;
   std::vector<long long> cnt((size_t)W, 0);
   long long* x = h->xch.p;
+  int64_t* x64 = reinterpret_cast<int64_t*>(x);
   for (long long left = n_samples; left > 0;) {
     const long long B = std::min<long long>(left, batch);
     const long long lo = sr_lo(B, r, W);
@@ -2531,22 +2605,19 @@ int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_
     if (int rc = round_sample(h, nullptr, nullptr, nb, lo, B)) return rc;
     // the round's goal lane: the lowest selecting lane of the whole round (k_sample's rule)
     hipLaunchKernelGGL(k_sr_put_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo, x);
-    if (int rc = tcmp_dist::allreduce_min_i64(c, reinterpret_cast<int64_t*>(x), 1, h->stream)) return rc;
+    if (int rc = X.min_i64(x64, 1, h->stream)) return rc;
     hipLaunchKernelGGL(k_sr_take_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo, nb, x);
     if (int rc = round_search(h, true, nb, B)) return rc;
     // accepted edges of every rank: this rank's insertion offset and the round's total
     hipLaunchKernelGGL(k_sr_put_count, dim3(1), dim3(1), 0, h->stream, h->st, x);
-    if (int rc = tcmp_dist::allgather_i64(c, reinterpret_cast<const int64_t*>(x + 1),
-                                         reinterpret_cast<int64_t*>(x + 3), 1, h->stream))
-      return rc;
+    if (int rc = X.allgather_i64(x64 + 1, x64 + 3, 1, h->stream)) return rc;
     hipLaunchKernelGGL(k_sr_take_counts, dim3(1), dim3(1), 0, h->stream, h->st, r, W, x);
     HIPCHK(hipMemcpyAsync(cnt.data(), x + 3, W * sizeof(long long), hipMemcpyDeviceToHost,
                           h->stream));
     if (int rc = round_write(h, nb)) return rc;
     // the lowest goal-reaching new node of the round
     hipLaunchKernelGGL(k_sr_put_goal, dim3(1), dim3(1), 0, h->stream, h->st, x);
-    if (int rc = tcmp_dist::allreduce_min_i64(c, reinterpret_cast<int64_t*>(x + 2), 1, h->stream))
-      return rc;
+    if (int rc = X.min_i64(x64 + 2, 1, h->stream)) return rc;
     hipLaunchKernelGGL(k_sr_take_goal, dim3(1), dim3(1), 0, h->stream, h->st, x);
     if (int rc = round_finish(h, nb)) return rc;
     HIPCHK(hipStreamSynchronize(h->stream));  // cnt
@@ -2566,7 +2637,7 @@ int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_
         }
         off += cnt[q];
       }
-      if (int rc = tcmp_dist::bcast_group(c, ops.data(), (int)ops.size(), h->stream)) return rc;
+      if (int rc = X.bcast(ops.data(), (int)ops.size(), h->stream)) return rc;
       T += all;
     }
     left -= B;
@@ -2574,109 +2645,147 @@ int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_
   return 0;
 }
 
+namespace {
+
+// Engines of one process on host threads: each exchange is a host barrier around device
+// copies (values through pinned host slots, node records peer to peer).  A failing engine
+// aborts the group so no thread waits on a barrier that can never fill.
+struct GroupState {
+  explicit GroupState(int n) : n(n), vals((size_t)n * 8), ops((size_t)n) {}
+  int n;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long long gen = 0;
+  bool aborted = false;
+  std::vector<int64_t> vals;                       // n x (up to 8) posted values
+  std::vector<const tcmp_dist::Bcast*> ops;        // each engine's broadcast list
+  int barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    if (aborted) return -1;
+    const long long g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return 0;
+    }
+    cv.wait(lk, [&] { return gen != g || aborted; });
+    return aborted ? -1 : 0;
+  }
+  void abort() {
+    std::lock_guard<std::mutex> lk(m);
+    aborted = true;
+    cv.notify_all();
+  }
+};
+
+class GroupExchange : public tcmp_dist::RoundExchange {
+ public:
+  GroupExchange(GroupState* g, int rank) : g_(g), r_(rank) {}
+  int rank() const override { return r_; }
+  int world() const override { return g_->n; }
+  int min_i64(int64_t* d, int n, hipStream_t s) override {
+    if (n > 8) return fail(-1, "group exchange: too many values");
+    if (int rc = post(d, n, s)) return rc;
+    std::vector<int64_t> m((size_t)n, LLONG_MAX);
+    for (int q = 0; q < g_->n; ++q)
+      for (int i = 0; i < n; ++i) m[i] = std::min(m[i], g_->vals[8 * q + i]);
+    if (g_->barrier()) return fail(-1, "group exchange aborted");  // all have read vals
+    HIPCHK(hipMemcpyAsync(d, m.data(), (size_t)n * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+  }
+  int allgather_i64(const int64_t* send, int64_t* recv, int n, hipStream_t s) override {
+    if (n > 8) return fail(-1, "group exchange: too many values");
+    if (int rc = post(send, n, s)) return rc;
+    std::vector<int64_t> all((size_t)g_->n * n);
+    for (int q = 0; q < g_->n; ++q)
+      for (int i = 0; i < n; ++i) all[(size_t)q * n + i] = g_->vals[8 * q + i];
+    if (g_->barrier()) return fail(-1, "group exchange aborted");
+    HIPCHK(hipMemcpyAsync(recv, all.data(), all.size() * sizeof(int64_t), hipMemcpyHostToDevice, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return 0;
+  }
+  int bcast(const tcmp_dist::Bcast* ops, int n_ops, hipStream_t s) override {
+    // the roots' ranges are final once every engine's stream has drained
+    HIPCHK(hipStreamSynchronize(s));
+    g_->ops[r_] = ops;
+    if (g_->barrier()) return fail(-1, "group exchange aborted");
+    for (int i = 0; i < n_ops; ++i) {
+      const int root = ops[i].root;
+      if (root == r_ || ops[i].bytes == 0) continue;
+      HIPCHK(hipMemcpyAsync(ops[i].ptr, g_->ops[root][i].ptr, ops[i].bytes, hipMemcpyDefault, s));
+    }
+    HIPCHK(hipStreamSynchronize(s));
+    // nobody reuses its list (or writes the ranges) before every copy has landed
+    if (g_->barrier()) return fail(-1, "group exchange aborted");
+    return 0;
+  }
+
+ private:
+  // this engine's n device values into its host slot, then wait for every engine's
+  int post(const int64_t* d, int n, hipStream_t s) {
+    int64_t v[8];
+    HIPCHK(hipMemcpyAsync(v, d, (size_t)n * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < n; ++i) g_->vals[8 * r_ + i] = v[i];
+    if (g_->barrier()) return fail(-1, "group exchange aborted");
+    return 0;
+  }
+  GroupState* g_;
+  int r_;
+};
+
+}  // namespace
+
+int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_t batch) {
+  if (int rc = set_dev(h)) return rc;
+  if (!c) return fail(-1, "null comm");
+  const int W = tcmp_dist::world(c);
+  if (W == 1) return tcmp_plan_run(h, n_samples, batch);
+  if (int rc = sr_check(h, n_samples, batch, W)) return rc;
+  tcmp_dist::RcclExchange X(c);
+  return shared_rounds(h, X, n_samples, batch);
+}
+
 int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch) {
   if (!hs || n < 1) return fail(-1, "bad arguments");
   if (n == 1) return tcmp_plan_run(hs[0], n_samples, batch);
   for (int q = 0; q < n; ++q) {
     if (!hs[q]) return fail(-1, "null handle");
+    for (int p = 0; p < q; ++p)
+      if (hs[p] == hs[q]) return fail(-1, "the same engine twice in a group");
     if (int rc = set_dev(hs[q])) return rc;
     if (int rc = sr_check(hs[q], n_samples, batch, n)) return rc;
     if (hs[q]->samples_issued != hs[0]->samples_issued)
       return fail(-1, "the engines' plans are not at the same round");
   }
-  long long T = 0;
-  if (int rc = set_dev(hs[0])) return rc;
-  if (int rc = sr_tree_size(hs[0], &T)) return rc;
-  std::vector<long long> v((size_t)n), cnt((size_t)n);
-  auto sync_all = [&]() -> int {
-    for (int q = 0; q < n; ++q) {
-      if (int rc = set_dev(hs[q])) return rc;
-      HIPCHK(hipStreamSynchronize(hs[q]->stream));
-    }
-    return 0;
-  };
-  // host-side exchange: slot `i` of every engine <- the minimum over the engines
-  auto host_min = [&](int i) -> int {
-    if (int rc = sync_all()) return rc;
-    long long m = LLONG_MAX;
-    for (int q = 0; q < n; ++q) {
-      if (int rc = set_dev(hs[q])) return rc;
-      HIPCHK(hipMemcpy(&v[q], hs[q]->xch.p + i, sizeof(long long), hipMemcpyDeviceToHost));
-      m = std::min(m, v[q]);
-    }
-    for (int q = 0; q < n; ++q) {
-      if (int rc = set_dev(hs[q])) return rc;
-      HIPCHK(hipMemcpy(hs[q]->xch.p + i, &m, sizeof(long long), hipMemcpyHostToDevice));
-    }
-    return 0;
-  };
-  for (long long left = n_samples; left > 0;) {
-    const long long B = std::min<long long>(left, batch);
-    auto lo = [&](int q) { return sr_lo(B, q, n); };
-    auto nbq = [&](int q) { return (int)(sr_lo(B, q + 1, n) - sr_lo(B, q, n)); };
-    for (int q = 0; q < n; ++q) {
-      tcmp_handle* h = hs[q];
-      if (int rc = set_dev(h)) return rc;
-      if (int rc = round_sample(h, nullptr, nullptr, nbq(q), lo(q), B)) return rc;
-      hipLaunchKernelGGL(k_sr_put_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo(q), h->xch.p);
-    }
-    if (int rc = host_min(0)) return rc;
-    for (int q = 0; q < n; ++q) {
-      tcmp_handle* h = hs[q];
-      if (int rc = set_dev(h)) return rc;
-      hipLaunchKernelGGL(k_sr_take_lane, dim3(1), dim3(1), 0, h->stream, h->st, lo(q), nbq(q),
-                         h->xch.p);
-      if (int rc = round_search(h, true, nbq(q), B)) return rc;
-      hipLaunchKernelGGL(k_sr_put_count, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
-    }
-    if (int rc = sync_all()) return rc;
-    for (int q = 0; q < n; ++q) {
-      if (int rc = set_dev(hs[q])) return rc;
-      HIPCHK(hipMemcpy(&cnt[q], hs[q]->xch.p + 1, sizeof(long long), hipMemcpyDeviceToHost));
-    }
-    for (int q = 0; q < n; ++q) {
-      tcmp_handle* h = hs[q];
-      if (int rc = set_dev(h)) return rc;
-      HIPCHK(hipMemcpy(h->xch.p + 3, cnt.data(), n * sizeof(long long), hipMemcpyHostToDevice));
-      hipLaunchKernelGGL(k_sr_take_counts, dim3(1), dim3(1), 0, h->stream, h->st, q, n, h->xch.p);
-      if (int rc = round_write(h, nbq(q))) return rc;
-      hipLaunchKernelGGL(k_sr_put_goal, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
-    }
-    if (int rc = host_min(2)) return rc;
-    for (int q = 0; q < n; ++q) {
-      tcmp_handle* h = hs[q];
-      if (int rc = set_dev(h)) return rc;
-      hipLaunchKernelGGL(k_sr_take_goal, dim3(1), dim3(1), 0, h->stream, h->st, h->xch.p);
-      if (int rc = round_finish(h, nbq(q))) return rc;
-    }
-    if (int rc = sync_all()) return rc;
-    long long all = 0;
-    for (long long c : cnt) all += c;
-    if (T + all <= hs[0]->P.max_nodes) {
-      long long off = T;
-      for (int q = 0; q < n; ++q) {
-        const size_t k = (size_t)cnt[q];
-        for (int p = 0; p < n && k; ++p) {
-          if (p == q) continue;
-          tcmp_handle* d = hs[p];
-          tcmp_handle* s = hs[q];
-          if (int rc = set_dev(d)) return rc;
-          HIPCHK(hipMemcpyAsync(d->cfg.p + 8 * off, s->cfg.p + 8 * off, k * 8 * sizeof(double),
-                                hipMemcpyDefault, d->stream));
-          HIPCHK(hipMemcpyAsync(d->tgt.p + 8 * off, s->tgt.p + 8 * off, k * 8 * sizeof(double),
-                                hipMemcpyDefault, d->stream));
-          HIPCHK(hipMemcpyAsync(d->parent.p + off, s->parent.p + off, k * sizeof(int),
-                                hipMemcpyDefault, d->stream));
-          HIPCHK(hipMemcpyAsync(d->meta.p + off, s->meta.p + off, k * sizeof(int2),
-                                hipMemcpyDefault, d->stream));
-        }
-        off += cnt[q];
+  GroupState g(n);
+  std::vector<int> rc((size_t)n, 0);
+  std::vector<std::string> err((size_t)n);
+  std::vector<std::thread> th;
+  th.reserve(n);
+  for (int q = 0; q < n; ++q)
+    th.emplace_back([&, q] {
+      GroupExchange X(&g, q);
+      int r = set_dev(hs[q]);
+      if (!r) r = shared_rounds(hs[q], X, n_samples, batch);
+      if (r) {
+        rc[q] = r;
+        err[q] = tcmp_last_error();  // the error string is thread-local
+        g.abort();
       }
-      if (int rc = sync_all()) return rc;
-      T += all;
-    }
-    left -= B;
-  }
+    });
+  for (auto& t : th) t.join();
+  // report the first engine that failed on its own (not one that only saw the abort)
+  int first = -1;
+  for (int q = 0; q < n; ++q)
+    if (rc[q] && err[q].find("aborted") == std::string::npos) { first = q; break; }
+  if (first < 0)
+    for (int q = 0; q < n; ++q)
+      if (rc[q]) { first = q; break; }
+  if (first >= 0) return fail(rc[first], "engine " + std::to_string(first) + ": " + err[first]);
   return 0;
 }
 

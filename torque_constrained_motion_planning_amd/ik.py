@@ -218,11 +218,26 @@ def sample_tool_ik(engine, tool_pose, current_conf, max_attempts=25, rng=None, s
     return None if not hits else hits[0]
 
 
-def bi_panda_inverse_kinematics(engine, gripper_pose, current_conf, collision_fn,
+def body_collision(engine, conf):
+    """any(pairwise_collision(robot, b) for b in obstacles) with the robot at `conf`
+    (franka_ik_fast.py:78, panda_primitives.py:260): body_collision -> get_closest_points at
+    the default max_distance = -MAX_DISTANCE (utils.py:2781,2833,2866-2880) over EVERY link of
+    the robot -- the moving links and the static base panda_link0 -- with no joint-limit test.
+    The scene is the one last given to `engine.set_scene`."""
+    hit = bool(engine.collides_body([conf])[0])
+    if hit:
+        print('body collision')  # utils.py:2877-2878
+    return hit
+
+
+def bi_panda_inverse_kinematics(engine, gripper_pose, current_conf, collision_fn=None,
                                 max_attempts=25, rng=None, shuffle=None):
     """franka_ik_fast.py:64-79.  Returns (conf or None, robot conf afterwards): the reference
     sets the joints to the IK solution before the collision check (:73), so a rejected
-    solution becomes the next attempt's current configuration."""
+    solution becomes the next attempt's current configuration.  collision_fn defaults to the
+    reference's body-level check (:78, `body_collision` above)."""
+    if collision_fn is None:
+        collision_fn = lambda q: body_collision(engine, q)  # noqa: E731
     conf = sample_tool_ik(engine, gripper_pose, current_conf, max_attempts=max_attempts, rng=rng,
                           shuffle=shuffle)
     if conf is None:
@@ -238,14 +253,12 @@ def grasp_conf_for_pose(problem, start_conf, pose, engine=None, rng=None, shuffl
     (point, quat) or 4x4), gripper pose, up to 25 IK attempts with the body collision check."""
     from ._lib import engine as get_engine
     from .scene import mesh_pack, obstacle_array
-    from .utils import get_collision_fn, get_arm_joints
 
     eng = get_engine() if engine is None else engine
     eng.set_scene(obstacle_array(problem.fixed), mesh_pack(problem.fixed))
     grasp = get_top_grasp(problem.payload)
     gripper_pose = multiply(from_matrix(to_matrix(pose)), invert(grasp.value))
-    collision_fn = get_collision_fn(problem.robot, get_arm_joints(problem.robot), problem.fixed,
-                                    self_collisions=False)
+    collision_fn = lambda q: body_collision(eng, q)  # noqa: E731  (franka_ik_fast.py:78)
     current = np.asarray(start_conf, dtype=np.float64)
     for _ in range(retries):
         conf, current = bi_panda_inverse_kinematics(eng, gripper_pose, current, collision_fn,

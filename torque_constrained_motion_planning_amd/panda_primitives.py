@@ -174,9 +174,14 @@ def planner_fn_force_aware(start_conf, pose, problem):
     resolutions = 0.2 ** np.ones(7)
     dynam_fn = get_dynamics_fn_v5(problem, resolutions)
     timestamp = str(datetime.datetime.now())
-    grasp_conf = grasp_conf_for_pose(problem, start_conf, pose)
-    collision_fn = get_collision_fn(robot, get_arm_joints(robot), obstacles, self_collisions=False)
-    if grasp_conf is None or collision_fn(grasp_conf):
+    from ._lib import engine as get_engine
+    from .ik import body_collision
+    from .scene import mesh_pack, obstacle_array
+    eng = get_engine()
+    grasp_conf = grasp_conf_for_pose(problem, start_conf, pose, engine=eng)
+    # any(pairwise_collision(robot, b) for b in obstacles) (:260): body level, link0 included
+    eng.set_scene(obstacle_array(obstacles), mesh_pack(obstacles))
+    if grasp_conf is None or body_collision(eng, grasp_conf):
         print('Grasp IK failure', grasp_conf)
         return None
     if not torque_test(grasp_conf):
