@@ -18,3 +18,5 @@ export TCMP_LIB_PATH=$PWD/torque_constrained_motion_planning_amd/libtcmp_asan.so
   LD_PRELOAD=$RT python -m pytest tests -m "not gpu" -q -p no:cacheprovider \
     --deselect tests/test_dist_gloo.py::test_gather_two_ranks_gloo 2>&1
 } | tee "$LOG"
+# the instrumented library is large and not used by any GPU run
+rm -f torque_constrained_motion_planning_amd/libtcmp_asan.so

@@ -753,47 +753,74 @@ __device__ __forceinline__ void minjerk_sample(const double* wp, long long nwp, 
   }
 }
 
-__device__ __forceinline__ bool torque_test_sample(int mode, double mass, const double q[7],
-                                                   const double qd[7], const double qdd[7]) {
-  if (mode == TCMP_TORQUE_BASE) return true;
-  double cq[7], sq[7];
-  for (int k = 0; k < 7; ++k) sincos(q[k], &sq[k], &cq[k]);
-  if (mode == TCMP_TORQUE_NOV) {
+// the planner's torque test on one sample (mode fixed per kernel instantiation), from cos /
+// sin of q computed once by the caller
+template <int MODE>
+__device__ __forceinline__ bool torque_test_m(double mass, const double cq[7], const double sq[7],
+                                              const double qd[7], const double qdd[7]) {
+  if constexpr (MODE == TCMP_TORQUE_BASE) return true;
+  if constexpr (MODE == TCMP_TORQUE_NOV) {
     const double z[7] = {0, 0, 0, 0, 0, 0, 0};
     return torque_ok<false>(cq, sq, z, z, mass);
   }
-  if (mode == TCMP_TORQUE_DYN) return torque_ok_dyn<true>(cq, sq, qd, qdd, mass);
+  if constexpr (MODE == TCMP_TORQUE_DYN) return torque_ok_dyn<true>(cq, sq, qd, qdd, mass);
   return torque_ok<true>(cq, sq, qd, qdd, mass);
 }
+__device__ __forceinline__ void sincos7(const double q[7], double cq[7], double sq[7]) {
+#pragma unroll
+  for (int k = 0; k < 7; ++k) sincos(q[k], &sq[k], &cq[k]);
+}
+// a kernel template instantiated per torque mode, picked on the host
+#define TCMP_BY_MODE(K, mode) \
+  ((mode) == TCMP_TORQUE_BASE ? K<TCMP_TORQUE_BASE> : (mode) == TCMP_TORQUE_NOV ? K<TCMP_TORQUE_NOV> \
+   : (mode) == TCMP_TORQUE_DYN ? K<TCMP_TORQUE_DYN> : K<TCMP_TORQUE_RNE>)
 
-// dynam_fn + final validation + Conf.torques for the planner's path (grid-stride)
-__global__ __launch_bounds__(256) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
-                                              double* oq, double* oqd, double* oqdd,
-                                              double* opsg, double* otau, long long kcap) {
-  const PlanParams P = *Pd;
+// dynam_fn + final validation for the planner's path, one row per thread; Conf.torques follow
+// in k_traj_tau (one RNE per kernel keeps both at two waves per SIMD)
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
+                       double* oq, double* oqd, double* oqdd, double* opsg, long long kcap) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (st->goal_node < 0) return;
   if (st->status != 0 && st->status != TCMP_PLAN_VALIDATION_FAILED) return;
   const long long K = st->K, ni = st->ni, W = st->W;
-  if (K > kcap) return;  // the host grows the rows and launches again
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < K;
-       i += (long long)gridDim.x * blockDim.x) {
-    double x[7], v[7], a[7];
-    minjerk_sample(wp, W, ni, i, x, v, a);
-    store7(oq + 7 * i, x);
-    store7(oqd + 7 * i, v);
-    store7(oqdd + 7 * i, a);
-    {
+  if (K > kcap || i >= K) return;  // K > kcap: the host grows the rows and launches again
+  const double exec_time = Pd->exec_time, mass = Pd->mass;
+  double x[7], v[7], a[7];
+  minjerk_sample(wp, W, ni, i, x, v, a);
+  store7(oq + 7 * i, x);
+  store7(oqd + 7 * i, v);
+  store7(oqdd + 7 * i, a);
+  {
 #pragma clang fp contract(off)
-      opsg[i] = (P.exec_time * (double)i) / (double)K;  // panda_primitives.py:315
-    }
-    if (!torque_test_sample(P.torque_mode, P.mass, x, v, a)) {
-      atomicMin(&st->first_fail, i);
-    }
-    double cq[7], sq[7], tau[7];
-    for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
-    rne<true>(cq, sq, v, a, 0.0, tau);  // Conf.torques: rne without payload (utils.py:3376)
-    store7(otau + 7 * i, tau);
+    opsg[i] = (exec_time * (double)i) / (double)K;  // panda_primitives.py:315
   }
+  double cq[7], sq[7];
+  sincos7(x, cq, sq);
+  if (!torque_test_m<MODE>(mass, cq, sq, v, a)) atomicMin(&st->first_fail, i);
+}
+
+// Conf.torques of the path's rows: rne without payload (utils.py:3376)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_traj_tau(const DevState* st, const double* q, const double* qd,
+                           const double* qdd, double* otau, long long kcap) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (st->goal_node < 0) return;
+  if (st->status != 0 && st->status != TCMP_PLAN_VALIDATION_FAILED) return;
+  const long long K = st->K;
+  if (K > kcap || i >= K) return;
+  double x[7], v[7], a[7], cq[7], sq[7], tau[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) x[k] = q[7 * i + k];
+  sincos7(x, cq, sq);
+  // the rates are loaded after the sin / cos (shorter live ranges: no spill)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int k = 0; k < 7; ++k) {
+    v[k] = qd[7 * i + k];
+    a[k] = qdd[7 * i + k];
+  }
+  rne<true>(cq, sq, v, a, 0.0, tau);
+  store7(otau + 7 * i, tau);
 }
 
 // first_fail uses LLONG_MAX as "none" during the kernel
@@ -830,18 +857,20 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
   if (act) collides[i] = c ? 1 : 0;
 }
 
-__global__ void k_torque(const double* q, const double* qd, const double* qdd, long long n,
-                         int mode, double mass, int* ok) {
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_torque(const double* q, const double* qd, const double* qdd, long long n,
+                         double mass, int* ok) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double x[7], v[7], a[7];
+  double x[7], v[7], a[7], cq[7], sq[7];
   load7(q + 8 * i, x);
   if (qd) load7(qd + 8 * i, v); else for (int k = 0; k < 7; ++k) v[k] = 0;
   if (qdd) load7(qdd + 8 * i, a); else for (int k = 0; k < 7; ++k) a[k] = 0;
-  ok[i] = torque_test_sample(mode, mass, x, v, a) ? 1 : 0;
+  sincos7(x, cq, sq);
+  ok[i] = torque_test_m<MODE>(mass, cq, sq, v, a) ? 1 : 0;
 }
 
-__global__ void k_rne(const double* q, const double* qd, const double* qdd, long long n,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_rne(const double* q, const double* qd, const double* qdd, long long n,
                       double mp, double* tau) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -867,21 +896,17 @@ __global__ void k_minjerk(const double* wp, long long nwp, long long ni, double*
   }
 }
 
-__global__ void k_validate(const double* q, const double* qd, const double* qdd, long long n,
-                           int mode, double mass, unsigned long long* first_fail, double* tau) {
+template <int MODE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_validate(const double* q, const double* qd, const double* qdd, long long n,
+                           double mass, unsigned long long* first_fail) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  double x[7], v[7], a[7];
+  double x[7], v[7], a[7], cq[7], sq[7];
   load7(q + 8 * i, x);
   load7(qd + 8 * i, v);
   load7(qdd + 8 * i, a);
-  if (!torque_test_sample(mode, mass, x, v, a)) atomicMin(first_fail, (unsigned long long)i);
-  if (tau) {
-    double cq[7], sq[7], t[7];
-    for (int k = 0; k < 7; ++k) sincos(x[k], &sq[k], &cq[k]);
-    rne<true>(cq, sq, v, a, 0.0, t);
-    store7(tau + 7 * i, t);
-  }
+  sincos7(x, cq, sq);
+  if (!torque_test_m<MODE>(mass, cq, sq, v, a)) atomicMin(first_fail, (unsigned long long)i);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2024,9 +2049,9 @@ int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const doub
   if (!rc && qdd) rc = upload7(h, h->s2, qdd, n);
   rc = rc ? rc : h->i0.ensure((size_t)n);
   if (rc) return rc;
-  hipLaunchKernelGGL(k_torque, dim3(grid_for(n, 128)), dim3(128), 0, h->stream, h->s0.p,
-                     qd ? h->s1.p : nullptr, qdd ? h->s2.p : nullptr, (long long)n,
-                     (int)torque_mode, payload_mass, h->i0.p);
+  hipLaunchKernelGGL(TCMP_BY_MODE(k_torque, torque_mode), dim3(grid_for(n, 256)), dim3(256), 0,
+                     h->stream, h->s0.p, qd ? h->s1.p : nullptr, qdd ? h->s2.p : nullptr,
+                     (long long)n, payload_mass, h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ok, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
@@ -2241,10 +2266,15 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
   rc = rc ? rc : h->u0.ensure(1);
   if (rc) return rc;
   HIPCHK(hipMemsetAsync(h->u0.p, 0xff, sizeof(unsigned long long), h->stream));
-  hipLaunchKernelGGL(k_validate, dim3(grid_for(n, 128)), dim3(128), 0, h->stream, h->s0.p,
-                     h->s1.p, h->s2.p, (long long)n, (int)torque_mode, payload_mass, h->u0.p,
-                     tau ? h->s3.p : nullptr);
+  hipLaunchKernelGGL(TCMP_BY_MODE(k_validate, torque_mode), dim3(grid_for(n, 256)), dim3(256), 0,
+                     h->stream, h->s0.p, h->s1.p, h->s2.p, (long long)n, payload_mass, h->u0.p);
   HIPCHK(hipGetLastError());
+  if (tau) {
+    // Conf.torques: rne without payload (utils.py:3376)
+    hipLaunchKernelGGL(k_rne, dim3(grid_for(n, 256)), dim3(256), 0, h->stream, h->s0.p, h->s1.p,
+                       h->s2.p, (long long)n, 0.0, h->s3.p);
+    HIPCHK(hipGetLastError());
+  }
   unsigned long long ff = 0;
   HIPCHK(hipMemcpyAsync(&ff, h->u0.p, sizeof(ff), hipMemcpyDeviceToHost, h->stream));
   if (tau)
@@ -2889,9 +2919,11 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
                      (long long)(h->wp.n / 7));
   auto launch_traj = [&]() {
     hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
-    hipLaunchKernelGGL(k_traj, dim3(std::min<unsigned>(grid_for(h->kcap, 256), 2048)), dim3(256), 0,
-                       h->stream, h->dP, h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p,
-                       h->ttau.p, h->kcap);
+    const dim3 gt(grid_for(h->kcap, 256));
+    hipLaunchKernelGGL(TCMP_BY_MODE(k_traj, h->P.torque_mode), gt, dim3(256), 0, h->stream, h->dP,
+                       h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p, h->kcap);
+    hipLaunchKernelGGL(k_traj_tau, gt, dim3(256), 0, h->stream, h->st, h->tq.p, h->tqd.p,
+                       h->tqdd.p, h->ttau.p, h->kcap);
     hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
   };
   launch_traj();
