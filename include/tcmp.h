@@ -242,6 +242,12 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch);
 /* retrace + dynam_fn min-jerk + final torque validation (rrt_star.py:199-211); fills result. */
 int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* result);
 
+/* retrace only (rrt_star.py:199-200, goal_n.retrace()): the finish for a caller whose own
+ * dynam_fn turns the waypoints into the trajectory (rrt_star.py:202 with a foreign dynam_fn).
+ * No min-jerk, no validation: status is 0 (goal found) or TCMP_PLAN_NO_GOAL, n_traj 0,
+ * first_fail -1; tcmp_plan_fetch then copies the waypoints. */
+int tcmp_plan_retrace(tcmp_handle* h, tcmp_plan_result* result);
+
 /* copy the finished plan: waypoints (n_waypoints x 7), trajectory q/qd/qdd (n_traj x 7),
  * psg (n_traj), tau = Conf.torques without payload (n_traj x 7).  Any pointer may be NULL. */
 int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,

@@ -263,6 +263,41 @@ def test_batched_frontier_vs_oracle(eng, batch, n_obs, mode, mass):
         assert r.status == ref["status"]
 
 
+@pytest.mark.parametrize("exec_time", [0.0, 1.0])
+def test_plan_retrace_only(eng, exec_time):
+    """tcmp_plan_retrace (the finish of a foreign dynam_fn): the same waypoints as
+    tcmp_plan_finish, no trajectory, status 0 even where the engine's min-jerk would assert
+    (execution time 0 -> zero intervals)."""
+    from torque_constrained_motion_planning_amd import _lib
+    rng = np.random.default_rng(77)
+    start = np.array([0, -np.pi / 4, 0.0, -6 * np.pi / 8, 0, np.pi / 2, np.pi / 4])
+    while True:
+        goal = start + rng.uniform(-0.4, 0.4, 7)
+        obs = boxes(rng, 8)
+        if not (O.collision(start, obs) or O.collision(goal, obs)) and O.torque_ok(goal, 2, 5.0):
+            break
+    eng.set_scene(obs)
+
+    def plan():
+        assert eng.plan_begin(start, goal, 2, 5.0, exec_time, max_nodes=2049, max_batch=256,
+                              seed=99) == 0
+        eng.plan_run(2048, 256)
+
+    plan()
+    rt = eng.plan_retrace()
+    assert rt.goal_found == 1 and rt.status == 0
+    assert rt.n_traj == 0 and rt.first_fail == -1 and rt.n_waypoints >= 2
+    wp = eng.plan_fetch(rt)["waypoints"]
+    plan()
+    fin = eng.plan_finish()
+    assert fin.goal_node == rt.goal_node and fin.n_waypoints == rt.n_waypoints
+    if exec_time == 0:
+        assert fin.status == _lib.PLAN_MINJERK_ASSERT and fin.n_traj == 0
+    else:
+        assert fin.status in (_lib.PLAN_OK, _lib.PLAN_VALIDATION_FAILED) and fin.n_traj > 0
+    assert np.array_equal(eng.plan_fetch(fin)["waypoints"], wp)
+
+
 # ---- goal IK (SURVEY §8 a13/a14) ------------------------------------------------------------
 def test_dyn_torque_test_host(eng):
     """get_torque_limits_not_exceded_test_v2 through the host mirror == the oracle."""

@@ -28,6 +28,7 @@ EXPORTS = [
     "tcmp_check_body", "tcmp_base_pd",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
+    "tcmp_plan_retrace",
     "tcmp_plan_run_shared", "tcmp_plan_run_group",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters",
@@ -126,6 +127,7 @@ def load_library(path=LIB_PATH):
                                           ctypes.c_int32]
         L.tcmp_plan_run.argtypes = [vp, ctypes.c_int64, ctypes.c_int32]
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
+        L.tcmp_plan_retrace.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
         L.tcmp_plan_debug_round.argtypes = [vp, ctypes.c_int64, _dp, _i32p, _dp, _i64p, _i32p]
@@ -402,6 +404,12 @@ class Engine:
     def plan_finish(self):
         r = PlanResult()
         self._check(self.L.tcmp_plan_finish(self.h, ctypes.byref(r)))
+        return r
+
+    def plan_retrace(self):
+        """tcmp_plan_retrace: the waypoints only (a foreign dynam_fn follows)."""
+        r = PlanResult()
+        self._check(self.L.tcmp_plan_retrace(self.h, ctypes.byref(r)))
         return r
 
     def plan_fetch(self, r):

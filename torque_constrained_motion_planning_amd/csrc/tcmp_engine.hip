@@ -1012,7 +1012,7 @@ struct tcmp_handle {
   DBuf<unsigned long long> nkeys_in, skeys, ckeys_in, ckeys;
   DBuf<int> nvals_in, svals, cvals_in, cperm;
   DBuf<double> stree, cbox;
-  DBuf<float> stree32;
+  DBuf<float> srow;  // the scan's first-pass node rows (32 B per node; tcmp_nn.h k_nn_rows)
   DBuf<float> cboxf, sboxf, bboxf;
   DBuf<int> chome, bcount, boff;
   DBuf<int> cflag, cid, cstart, sflag, sid, sstart;
@@ -1205,7 +1205,7 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
   rc = rc ? rc : h->nvals_in.ensure(N);
   rc = rc ? rc : h->svals.ensure(N);
   rc = rc ? rc : h->stree.ensure(N * 8);
-  rc = rc ? rc : h->stree32.ensure(N * 8);
+  rc = rc ? rc : h->srow.ensure(N * 8);
   rc = rc ? rc : h->cboxf.ensure((N + 1) * 16);  // worst case: one cell per node
   rc = rc ? rc : h->sboxf.ensure((N + 1) * 16);
   rc = rc ? rc : h->bboxf.ensure((N / 64 + 2) * 16);
@@ -1306,7 +1306,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
                                              kKeyBits, h->stream));
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, st,
-                     cfg, h->svals.p, h->stree.p, h->stree32.p, T_bound, h->cflag.p, h->sflag.p);
+                     dP, cfg, h->svals.p, h->stree.p, h->srow.p, T_bound, h->cflag.p, h->sflag.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_nn_cut<kNnC>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
                      &st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
@@ -1369,7 +1369,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   h->mark_begin(F_NNSCAN, &e0);
 #define TCMP_NNW(UWV, SWV)                                                                   \
   hipLaunchKernelGGL((k_nearest_wave32<UWV, SWV>), dim3(blocks), dim3(kNnBlock), 0, h->stream, dP, st, \
-                     h->stree.p, h->stree32.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,          \
+                     h->stree.p, h->srow.p, h->cboxf.p, h->sboxf.p, h->bboxf.p, cand,             \
                      h->cperm.p, h->chome.p, nb, nn, second, score)
   // two cells per scan round: same-box A/B of 1 / 2 / 3 / 4 / 5 gave 4.44 / 4.03 / 4.21 /
   // 4.23 / 4.27 ms of scan per C3 query (eight: 137 VGPRs cost a wave per SIMD)
@@ -1601,7 +1601,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->cs_hoff.release();
   for (auto* b : {&h->nvals_in, &h->svals, &h->cvals_in, &h->cperm}) b->release();
   h->stree.release();
-  h->stree32.release();
+  h->srow.release();
   h->cbox.release();
   h->cboxf.release();
   h->sboxf.release();
@@ -2421,7 +2421,7 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
                         (const void*)h->nsteps.p, (const void*)h->nbr.p, (const void*)h->ncount.p,
                         (const void*)h->second.p, (const void*)h->rwlist.p, (const void*)h->nnscore.p,
                         (const void*)h->nkeys_in.p, (const void*)h->skeys.p, (const void*)h->nvals_in.p,
-                        (const void*)h->svals.p, (const void*)h->stree.p, (const void*)h->stree32.p,
+                        (const void*)h->svals.p, (const void*)h->stree.p, (const void*)h->srow.p,
                         (const void*)h->cboxf.p, (const void*)h->sboxf.p, (const void*)h->bboxf.p,
                         (const void*)h->cflag.p, (const void*)h->cid.p, (const void*)h->cstart.p,
                         (const void*)h->sflag.p, (const void*)h->sid.p, (const void*)h->sstart.p,
@@ -2904,7 +2904,8 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
   return 0;
 }
 
-int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
+// traj = false: retrace only (tcmp_plan_retrace, a foreign dynam_fn takes the waypoints)
+static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   if (int rc = set_dev(h)) return rc;
   if (!r) return fail(-1, "null result");
   if (!h->plan_open) return fail(-1, "no open plan");
@@ -2926,7 +2927,7 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
                        h->tqdd.p, h->ttau.p, h->kcap);
     hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
   };
-  launch_traj();
+  if (traj) launch_traj();
   HIPCHK(hipGetLastError());
   h->mark_end(F_FINISH, e0);
   DevState& s = h->pin->st;
@@ -2938,7 +2939,12 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   h->fin_K = 0;
   if (s.goal_node >= 0) {
     if (s.status == -3) return fail(-3, "waypoint capacity exceeded");
-    if (s.K > h->kcap) {
+    if (!traj) {
+      // no min-jerk ran: the retrace's own K / status (MINJERK_ASSERT) describe nothing
+      s.K = 0;
+      s.status = 0;
+      s.first_fail = -1;
+    } else if (s.K > h->kcap) {
       // an execution time past the preallocated rows: grow and run the trajectory again
       const long long K = s.K;
       int rc = h->tq.ensure(K * 7);
@@ -2984,6 +2990,10 @@ int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) {
   r->nn_full_pairs = s.nn_full_pairs;
   return 0;
 }
+
+int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) { return plan_finish_impl(h, r, true); }
+
+int tcmp_plan_retrace(tcmp_handle* h, tcmp_plan_result* r) { return plan_finish_impl(h, r, false); }
 
 int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
                     double* psg, double* tau) {

@@ -1,16 +1,24 @@
-// tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with an fp32
-// first pass.  Included by tcmp_engine.hip after tcmp_nn.h.
+// tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with a
+// 16-bit first pass.  Included by tcmp_engine.hip after tcmp_nn.h.
 //
-// Every (candidate, node) pair is first evaluated in fp32 on stree32 (half the bytes of the
-// fp64 rows, twice the VALU rate).  A node is re-evaluated exactly in fp64 (the same
-// arithmetic as k_nearest_wave, so the winner and its distance are bit-identical) only when
-// its fp32 value r32 could belong to a node at least as close as the wave's current best m:
+// Every (candidate, node) pair is first evaluated in fp32 on the f32 rows srow (half the bytes
+// of the fp64 rows, twice the VALU rate).  A node is re-evaluated exactly in fp64 (the same
+// arithmetic as the reference's distance fn, so the winner and its distance are bit-identical)
+// only when its fp32 value r32 could belong to a node at least as close as the wave's current
+// best m:
 //
 //   |q| <= cmax (P.nn_cmax: 8 > the joint-limit magnitude 3.7525 on the planner's path; the
 //   data's own bound for tcmp_nearest), so each fp32 coordinate difference is within
 //   e = 4 u cmax of the exact one (u = 2^-24), and with
 //   D = exact weighted distance, E = e sqrt(sum w):   r32 <= (1 + g) (D + E)^2,  g = 16 u.
 //   Refine iff r32 <= R(m) = (1 + g)(sqrt(m) + E)^2 (rounded up, with slack).
+//
+// TCMP_NN_Q16 builds (tcmp_nn.h: measured slower, kept as a knob) read 16-bit rows instead
+// (g_k = (x_k + cm) / qs rounded, qs = 2 cm / 65534 with cm the f32 coordinate bound) as
+// d_k = fma(g_k, -qs, o_k), o_k = fl(s32_k + cm) once per candidate; each d_k is then within
+// e = 6 u cmax + 0.5000001 qs of the exact difference (s32 and o_k roundings 3 u cmax, the
+// fma's rounding <= u |d| <= 3 u cmax, quantization qs / 2 plus the build quotient's fp64
+// noise), the same model with the larger e.
 //
 // Nodes that are not refined feed the second-smallest distance through the matching lower
 // bound LB(r32) = (sqrt(r32 / (1 + g)) - E)^2, so `second` is a lower bound of the exact value:
@@ -114,7 +122,7 @@ template <bool UW, int SW>
 #endif
 __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
-                                                        const float* stree32, const float* cbox,
+                                                        const float* srow, const float* cbox,
                                                         const float* sbox, const float* bbox,
                                                         const double* cand,
                                                         const int* cperm, const int* home, int nb,
@@ -139,7 +147,13 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     w32[k] = (float)w[k];
     wsum += w[k];
   }
+#if TCMP_NN_Q16
+  const float qcm = nn_qcm(P.nn_cmax), qs = nn_qstep(qcm);
+  const double E = (6.0 * kNnU32 * P.nn_cmax + 0.5000001 * (double)qs) *
+                   sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
+#else
   const double E = 4.0 * kNnU32 * P.nn_cmax * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
+#endif
   const float G = (float)(8.0 * kNnU32 * P.nn_cmax);  // box_lb32's coordinate shift
   const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
 #ifndef TCMP_NN_RWPAD
@@ -211,6 +225,9 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
 #pragma unroll
     for (int k = 0; k < 7; ++k) s[k] = readlane_d(sl[k], ib);
     float s32[7], sh[7], sl32[7];
+#if TCMP_NN_Q16
+    float so[7];
+#endif
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       // wave-uniform: readfirstlane puts them back in SGPRs (the VALU arithmetic leaves them
@@ -218,6 +235,9 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
       s32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)s[k])));
       sh[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] + G)));
       sl32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] - G)));
+#if TCMP_NN_Q16
+      so[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] + qcm)));
+#endif
     }
     const int hc = __builtin_amdgcn_readlane(hml, ib);
     const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
@@ -255,13 +275,28 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     };
     // packed fp32 (v_pk_add / v_pk_fma: two joints per instruction); any association of the
     // seven terms stays inside the error model's g = 16 u
-    const f32x2 s01 = {s32[0], s32[1]}, s23 = {s32[2], s32[3]}, s45 = {s32[4], s32[5]},
-                s6 = {s32[6], 0.f};
     const f32x2 w01 = {w32[0], w32[1]}, w23 = {w32[2], w32[3]}, w45 = {w32[4], w32[5]},
                 w6 = {w32[6], 0.f};
+#if TCMP_NN_Q16
+    // a 16-bit row against the candidate's grid offsets so: d = so - g qs
+    const float nqs = -qs;
+    auto dist32 = [&](const uint4 R) {
+      const float* o = so;
+      const f32x2 n2 = {nqs, nqs};
+      const f32x2 d01 = __builtin_elementwise_fma(
+          f32x2{(float)(R.x & 0xffffu), (float)(R.x >> 16)}, n2, f32x2{o[0], o[1]});
+      const f32x2 d23 = __builtin_elementwise_fma(
+          f32x2{(float)(R.y & 0xffffu), (float)(R.y >> 16)}, n2, f32x2{o[2], o[3]});
+      const f32x2 d45 = __builtin_elementwise_fma(
+          f32x2{(float)(R.z & 0xffffu), (float)(R.z >> 16)}, n2, f32x2{o[4], o[5]});
+      const f32x2 d6 = {fmaf((float)R.w, nqs, o[6]), 0.f};
+#else
+    const f32x2 s01 = {s32[0], s32[1]}, s23 = {s32[2], s32[3]}, s45 = {s32[4], s32[5]},
+                s6 = {s32[6], 0.f};
     auto dist32 = [&](const float4 a, const float4 b) {
       const f32x2 d01 = s01 - f32x2{a.x, a.y}, d23 = s23 - f32x2{a.z, a.w},
                   d45 = s45 - f32x2{b.x, b.y}, d6 = s6 - f32x2{b.z, 0.f};
+#endif
       f32x2 acc;
       if (UW) {
         acc = d01 * d01;
@@ -290,19 +325,27 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     };
     // up to SW cells (count 0 = none), all row loads in flight before any use
     auto scanw = [&](const int cs[SW], const int cn[SW]) -> void {
+#if TCMP_NN_Q16
+      uint4 R[SW];
+#else
       float4 A[SW], Bq[SW];
+#endif
       bool val[SW];
 #pragma unroll
       for (int u = 0; u < SW; ++u) {
         // wave-uniform row base + lane offset
         const int c0 = __builtin_amdgcn_readfirstlane(cs[u]);
         const int cnt = __builtin_amdgcn_readfirstlane(cn[u]);
-        const float4* rp = reinterpret_cast<const float4*>(stree32) + 2 * (unsigned)c0;
         val[u] = lane < cnt;
+#if TCMP_NN_Q16
+        if (val[u]) R[u] = reinterpret_cast<const uint4*>(srow)[(unsigned)c0 + lane];
+#else
+        const float4* rp = reinterpret_cast<const float4*>(srow) + 2 * (unsigned)c0;
         if (val[u]) {
           A[u] = rp[2 * lane];
           Bq[u] = rp[2 * lane + 1];
         }
+#endif
         pairs += (unsigned long long)cnt;
       }
       // the SW distances first, then one branch: refinement (r <= Rf) is the rare case
@@ -310,7 +353,11 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
       float rm = INFINITY;
 #pragma unroll
       for (int u = 0; u < SW; ++u) {
+#if TCMP_NN_Q16
+        r[u] = val[u] ? dist32(R[u]) : INFINITY;
+#else
         r[u] = val[u] ? dist32(A[u], Bq[u]) : INFINITY;
+#endif
         rm = fminf(rm, r[u]);
       }
       if (rm <= Rf) {

@@ -87,9 +87,9 @@ def _validate_and_return(rrt_path, dynam_fn, torque_fn, native_torque):
 
 def _finish(eng, dynam_fn=None, torque_fn=None):
     """tcmp_plan_finish -> the reference's return tuple.  dynam_fn: a foreign dynamics fn,
-    applied on the host to the engine's retraced waypoints (else the engine's min-jerk and
-    validation stand)."""
-    r = eng.plan_finish()
+    applied on the host to the engine's retraced waypoints (tcmp_plan_retrace: no device
+    min-jerk or validation runs for it); else the engine's min-jerk and validation stand."""
+    r = eng.plan_retrace() if dynam_fn is not None else eng.plan_finish()
     if r.status == _lib.PLAN_NO_GOAL:
         print("failed to find goal")
         return (None, None, None, None), r, None
@@ -121,7 +121,7 @@ def _rrt_engine(start, goal, distance, sample, extend, collision, torque_fn, dyn
     start = tuple(float(x) for x in start)
     goal = tuple(float(x) for x in goal)
     st = eng.plan_begin(start, goal, torque_fn.mode, torque_fn.payload_mass,
-                        dynam_fn.execution_time if native_dynam else 5.0,
+                        dynam_fn.execution_time if native_dynam else 0.0,
                         max_nodes=max_iterations + 1, max_batch=1,
                         weights=distance.weights, resolutions=extend.resolutions,
                         radius=_radius_value(radius), goal_probability=goal_probability)
