@@ -58,6 +58,32 @@ def pmc_traffic(kernel, workload):
     return (2 * sum(fetch) + sum(write)) * 1024 / len(fetch)
 
 
+def pmc_valu(kernel, workload, peak, counters=("SQ_INSTS_VALU_FLOPS_FP64",)):
+    """Measured VALU flop of `kernel` from the newest committed PMC summary of THIS workload
+    (profiles/<tag>_pmc_valu_<workload>.json: a rocprofv3 --pmc pass of the SQ_INSTS_VALU_*
+    counters over one bench step): flop per launch (summed over `counters`, averaged over the
+    step's launches) and the rate over the same dispatches' traced durations.  None when the
+    workload was never profiled that way."""
+    prof = os.path.join(REPO, "profiles")
+    suffix = "_pmc_valu_%s.json" % workload
+    pmc = sorted(f for f in os.listdir(prof) if f.endswith(suffix)) if os.path.isdir(prof) else []
+    if not pmc:
+        return None
+    d = json.load(open(os.path.join(prof, pmc[-1])))["dispatches"].get(kernel, [])
+    rows = [x for x in d if x["counter"] == counters[0]]
+    if not rows:
+        return None
+    # SQ_INSTS_VALU_FLOPS_* count flop per wave instruction (they equal 2 FMA + ADD + MUL of
+    # the SQ_INSTS_VALU_*_F64 instruction counts): x 64 lanes, exec-masked lanes included, so
+    # an upper bound of the lanes' own flop
+    flop = 64.0 * sum(x["value_KiB"] for x in d if x["counter"] in counters)
+    us = sum(x["dur_us"] or 0.0 for x in rows)
+    tf = flop / (us * 1e-6) / 1e12 if us > 0 else None
+    return {"flop_per_launch": flop / len(rows), "tflops_traced": tf,
+            "frac_traced": tf / peak if tf else None, "counters": list(counters),
+            "source": "profiles/" + pmc[-1]}
+
+
 # BASELINE.json configs (SURVEY 8 sizes): boxes, meshes, torque test, payload, samples per
 # query, queries per step (all ranks together), scaling.  Batch per round: SURVEY 8d's
 # 65,536 for the 1e5-sample queries (C2 17.4M -> 28.0M, C4 26.7M -> 39.7M samples/s over
@@ -396,6 +422,8 @@ def main():
         "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, scans),
         "bound": "valu_fp32", "achieved": nn_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
         "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32", args.workload),
+        "measured_valu": pmc_valu("k_nearest_wave32", args.workload, PEAK_FP32_TFLOPS,
+                                  ("SQ_INSTS_VALU_FLOPS_FP32",)),
         "algorithmic": "%d flop per evaluated (candidate, node) pair; %d pairs over %d launches "
                        "(brute force would be %d pairs: %.1f PFLOP/s equivalent)" % (
                            NN_FLOP_PER_PAIR, nn_pairs, scans, nn_full,
@@ -412,10 +440,19 @@ def main():
         "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
         "bound": "valu_fp64", "achieved": ed_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
         "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges", args.workload),
+        # the hardware's own count of the kernel's fp64 VALU flop (PMC), beside the SURVEY 8d
+        # contract flop above
+        "measured_valu": pmc_valu("k_edges", args.workload, PEAK_FP64_TFLOPS),
         "algorithmic": "per extend step F_fk %d + F_bp %d x %d links x %d obstacles + F_rne %d, "
                        "+ F_sat %d per pair past the cull; %d steps, %d such pairs, %d launches" % (
                            F_FK, F_BP, N_LINKS, n_obs_total, f_rne, F_SAT, steps, sat,
                            launches)}
+    for roof, peak in ((roof_nn, PEAK_FP32_TFLOPS), (roof_ed, PEAK_FP64_TFLOPS)):
+        mv = roof["measured_valu"]
+        if mv and roof["avg_launch_ms"] > 0:
+            # the PMC flop per launch over this run's event-timed average launch
+            mv["tflops_live"] = mv["flop_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
+            mv["frac_live"] = mv["tflops_live"] / peak
     dominant, other = (roof_nn, roof_ed) if nn_ms >= ed_ms else (roof_ed, roof_nn)
     # north-star HBM figure: compulsory bytes per query = 68 T_r per round (tree read
     # once) + 72 B_r per round (candidates written) + trajectory rows, over the step time

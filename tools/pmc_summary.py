@@ -38,6 +38,7 @@ def main():
                     disp.setdefault(k, []).append({
                         "counter": row.get("Counter_Name"),
                         "grid": int(float(row.get("Grid_Size", 0) or 0)),
+                        # the raw counter value (KiB for FETCH_SIZE / WRITE_SIZE)
                         "value_KiB": float(row.get("Counter_Value", 0) or 0),
                         "dur_us": (end - start) / 1e3 if end > start else None,
                     })
