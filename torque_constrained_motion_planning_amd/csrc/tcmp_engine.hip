@@ -351,10 +351,20 @@ struct EdgeJob {
   int* accepted;            // nullable: accepted edges (nsafe > 0) per 256 edges, cleared before
 };
 
+#ifndef TCMP_EDGE_SPLIT
+#define TCMP_EDGE_SPLIT 4  // small rounds: up to this many lanes per edge (k_edges SPLIT)
+#endif
 #ifndef TCMP_EDGE_MINW
 #define TCMP_EDGE_MINW 2  // min waves per SIMD the register allocation must allow
 #endif
-template <bool MESH>
+// SPLIT = 2 or 4 (rounds with at most a half / a quarter of the resident lanes' edges, e.g.
+// C2's 65,536 and 34,464): SPLIT adjacent lanes share an edge and check SPLIT consecutive
+// steps at a time -- lane k of the group step i + k, its configuration reached by the same
+// k + 1 refine steps (so the same bits) -- and the edge advances past the passing prefix and
+// ends at the first failing step, exactly the sequential walk's result; the checks past a
+// failure are wasted only in an edge's last iteration.  The counted extend steps are the
+// sequential walk's (nsafe + 1 on a failure, else n).
+template <bool MESH, int SPLIT>
 __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const PlanParams* __restrict__ Pd, Scene sc_g, Geo g_g,
                                                DevState* st) {
   const PlanParams P = *Pd;
@@ -363,6 +373,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
   Geo g;
   stage_lds<!MESH>(sc_g, g_g, tcmp_lds, sc, g);
   const int lane = lane_id();
+  const int sub = lane & (SPLIT - 1);  // position in the lane group of an edge
   int e = -1, i = 0, n = 0;
   bool done = false;
   double q[7];  // last safe configuration of the lane's edge (the target is re-read per step)
@@ -382,14 +393,15 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
     unsigned long long c0 = clock64();
 #endif
     const bool need = !done && e < 0;
-    const uint64_t m = __ballot(need);
+    const uint64_t m = __ballot(need && sub == 0);
     if (m) {
       const int leader = __builtin_ctzll(m);
       int base = 0;
       if (lane == leader) base = atomicAdd(&st->work_counter, (int)__popcll(m));
       base = __shfl(base, leader);
       if (need) {
-        const int my = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+        // (the other lanes of a group take its first lane's slot: all hold the same edge)
+        const int my = base + (int)__popcll(m & ((1ull << (lane - sub)) - 1ull));
         if (my < J.n) {
           e = J.order ? J.order[my] : my;
           const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
@@ -407,7 +419,8 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_fetch += c1 - c0; c0 = c1; }
 #endif
-    const bool active = e >= 0;
+    // lane k of a group checks step i + k (none past the edge's last step)
+    const bool active = e >= 0 && (SPLIT == 1 || i + sub < n);
     // The step's configuration qn, its sin/cos and the torque test come first; during the
     // collision check only q (the last safe configuration) and cq/sq stay live -- the target
     // q2 is re-read from memory and qn regenerated (the same arithmetic, so the same bits)
@@ -421,6 +434,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
       if (active) {
         load7(J.to + 8 * (size_t)e, q2);
         refine_step(qn, q2, n, i);
+        for (int k = 1; k <= sub; ++k) refine_step(qn, q2, n, i + k);
       }
 #pragma unroll
       for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
@@ -446,20 +460,47 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
     { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
 #endif
     const bool ok = active && !coll && tok;
-    if (active) {
-      ++steps;
-      if (ok) {
-        double q2[7];
-        load7(J.to + 8 * (size_t)e, q2);
-        refine_step(q, q2, n, i);
-        ++i;
+    if (SPLIT == 1) {
+      if (active) {
+        ++steps;
+        if (ok) {
+          double q2[7];
+          load7(J.to + 8 * (size_t)e, q2);
+          refine_step(q, q2, n, i);
+          ++i;
+        }
+        if (!ok || i == n) {
+          if (J.accepted && i > 0) atomicAdd(&J.accepted[e >> 8], 1);
+          J.nsafe[e] = i;
+          J.nsteps[e] = n;
+          store7(J.last + 8 * (size_t)e, q);
+          e = -1;
+        }
       }
-      if (!ok || i == n) {
-        if (J.accepted && i > 0) atomicAdd(&J.accepted[e >> 8], 1);
-        J.nsafe[e] = i;
-        J.nsteps[e] = n;
-        store7(J.last + 8 * (size_t)e, q);
-        e = -1;
+    } else {
+      // the group's verdicts: it advances past its passing prefix (all lanes reach the ballot)
+      const uint64_t okm = __ballot(ok);
+      const unsigned gb = (unsigned)(okm >> (lane - sub)) & ((1u << SPLIT) - 1u);
+      if (e >= 0) {
+        const int na = min(SPLIT, n - i);               // steps the group checked
+        const int adv = min(__builtin_ctz(~gb), na);    // passing prefix
+        if (adv) {
+          double q2[7];
+          load7(J.to + 8 * (size_t)e, q2);
+          for (int k = 0; k < adv; ++k) refine_step(q, q2, n, i + k);
+          i += adv;
+        }
+        const bool failed = adv < na;
+        if (failed || i == n) {
+          if (sub == 0) {
+            steps += (unsigned)(failed ? i + 1 : n);
+            if (J.accepted && i > 0) atomicAdd(&J.accepted[e >> 8], 1);
+            J.nsafe[e] = i;
+            J.nsteps[e] = n;
+            store7(J.last + 8 * (size_t)e, q);
+          }
+          e = -1;
+        }
       }
     }
 #ifdef TCMP_PROF
@@ -1058,6 +1099,7 @@ struct tcmp_handle {
   long long launches_nearest = 0;
   long long launches_scan = 0;      // k_nearest_wave32 launches of the open plan
   int edge_blocks = 0;
+  int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
 
   Geo geo() const {
     return Geo{verts.p, planes.p, edges.p, verts32.p,
@@ -1421,7 +1463,18 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool re
   blocks = std::min(blocks, cap);
   blocks = std::max<long long>(blocks, 1);
   h->edge_blocks = (int)blocks;
-  hipLaunchKernelGGL(h->mesh_kernels() ? k_edges<true> : k_edges<false>, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, dP,
+  // a round with at most a half / a quarter of the resident lanes' edges: two / four lanes
+  // per edge (k_edges SPLIT)
+  int split = 1;
+  while (split < std::min(TCMP_EDGE_SPLIT, h->edge_split) && 2LL * split * J.n <= cap * 256)
+    split *= 2;
+  if (split > 1) blocks = std::min(cap, ((long long)split * J.n + 255) / 256);
+  h->edge_blocks = (int)blocks;
+  const bool mk = h->mesh_kernels();
+  auto kern = split == 4 ? (mk ? k_edges<true, 4> : k_edges<false, 4>)
+              : split == 2 ? (mk ? k_edges<true, 2> : k_edges<false, 2>)
+                           : (mk ? k_edges<true, 1> : k_edges<false, 1>);
+  hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(256), lds_bytes(h), h->stream, J, dP,
                      h->scene(), h->geo(), h->st);
   HIPCHK(hipGetLastError());
   return 0;
@@ -1551,7 +1604,9 @@ int tcmp_create(int device, tcmp_handle** out) {
     }
     // dynamic LDS above 64 KiB per workgroup must be allowed explicitly
     const int lim = (int)stage_lds_bytes(kMaxObstacles);
-    for (const void* k : {(const void*)k_edges<false>, (const void*)k_edges<true>,
+    for (const void* k : {(const void*)k_edges<false, 1>, (const void*)k_edges<true, 1>,
+                          (const void*)k_edges<false, 2>, (const void*)k_edges<true, 2>,
+                          (const void*)k_edges<false, 4>, (const void*)k_edges<true, 4>,
                           (const void*)k_check_configs<false>, (const void*)k_check_configs<true>,
                           (const void*)k_rewire_apply<false>, (const void*)k_rewire_apply<true>})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
@@ -1566,6 +1621,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
   if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(16, std::max(8, atoi(e)));
+  if (const char* e = getenv("TCMP_EDGE_SPLIT")) h->edge_split = std::max(1, std::min(4, atoi(e)));
   if (const char* e = getenv("TCMP_NN_CSORT")) h->nn_cand_count_bits = std::min(16, std::max(0, atoi(e)));
   *out = h;
   return 0;
@@ -2413,6 +2469,7 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
   mix((unsigned long long)lds_bytes(h));
   mix((unsigned long long)h->nn_waves_per_cu);
   mix((unsigned long long)h->nn_cand_bits);
+  mix((unsigned long long)h->edge_split);
   mix((unsigned long long)h->nn_cand_count_bits);
   mix((unsigned long long)h->sort_tmp.n);
   for (const void* p : {(const void*)h->cfg.p, (const void*)h->tgt.p, (const void*)h->parent.p,
