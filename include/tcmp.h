@@ -89,6 +89,15 @@ typedef struct tcmp_hulls {
 int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls* outer,
                        int32_t n_mesh);
 
+/* Optional inscribed spheres for the current meshes (call after tcmp_set_meshes; cleared by
+ * it): spheres[n_mesh][k][4] = (cx, cy, cz, r), world frame, each ball inside mesh m's hull;
+ * k must be 16.  Like the LODs they are certificates only (same reference semantics,
+ * utils.py:2833 closest points at -0.04): a link sphere and a mesh sphere overlapping by
+ * >= 0.04 + 1e-4 prove "collision", and the full hulls' projections on the direction between
+ * the most-overlapping pair's centres overlapping by < 0.04 - 1e-4 prove "free".  Results do
+ * not depend on them -- only speed.  spheres.py builds them. */
+int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh, int32_t k);
+
 /* Self-collision (get_collision_fn(..., self_collisions=True), utils.py:3165-3191 with the
  * pairs of get_self_link_pairs, utils.py:3125-3149): enable != 0 adds the 33 link pairs of
  * the arm whose moving-ancestor joint sets differ and that are not parent/child (link0 is the

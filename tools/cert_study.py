@@ -1,0 +1,203 @@
+#!/usr/bin/env python3
+"""CPU study of cheap per-pair certificates for the C5 exact link-vs-mesh tests.
+
+Samples configurations, finds the (link, mesh) pairs that reach the exact stage (tier 0 AABB
+overlap >= 0.04, outer-OBB SAT >= 0.04, inner-box SAT < 0.04), computes their exact depth with
+the oracle, and reports how many each candidate certificate decides:
+
+  * sphere collision certificate: inscribed spheres of both hulls, collision if some sphere pair
+    overlaps by >= 0.04 + guard (depth is monotone under inclusion);
+  * outer-LOD free (the kernel's current second stage) for reference.
+
+usage: python tools/cert_study.py [n_configs] [K]
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+
+import oracle as O  # noqa: E402
+from torque_constrained_motion_planning_amd import hull  # noqa: E402
+from torque_constrained_motion_planning_amd.spheres import inscribed_spheres  # noqa: E402
+
+PEN = 0.04
+LO = np.array([-2.8973, -1.7628, -2.8973, -3.0718, -2.8973, -0.0175, -2.8973])
+HI = np.array([2.8973, 1.7628, 2.8973, -0.0698, 2.8973, 3.7525, 2.8973])
+
+
+def scene():
+    path = "/tmp/c5_scene.npz"
+    import bench
+    from gen_fullsize import OracleEngine
+    eng = OracleEngine()
+    t0 = time.time()
+    obs, pack, goal = bench.make_query(1234, n_obs=0, mode=2, mass=5.0, engine=eng, n_mesh=256)
+    print("scene %.0f s" % (time.time() - t0), flush=True)
+    return pack
+
+
+def obb_sat(ca, Ra, ha, cb, Rb, hb):
+    """min over the 15 OBB axes of the projection overlap (R columns = box axes)."""
+    axes = [Ra[:, i] for i in range(3)] + [Rb[:, i] for i in range(3)]
+    for i in range(3):
+        for j in range(3):
+            a = np.cross(Ra[:, i], Rb[:, j])
+            n = np.linalg.norm(a)
+            if n > 1e-9:
+                axes.append(a / n)
+    best = np.inf
+    d = cb - ca
+    for a in axes:
+        ra = np.sum(ha * np.abs(Ra.T @ a))
+        rb = np.sum(hb * np.abs(Rb.T @ a))
+        best = min(best, ra + rb - abs(d @ a))
+    return best
+
+
+def main():
+    n_cfg = int(sys.argv[1]) if len(sys.argv) > 1 else 300
+    K = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    pack = scene()
+    O.set_meshes(pack)
+    g = np.load(os.path.join(REPO, "torque_constrained_motion_planning_amd", "data", "panda_geometry.npz"))
+    lverts = [g["verts"][g["vert_off"][i]:g["vert_off"][i + 1]] for i in range(10)]
+    lboxes = g["boxes"]
+    # link spheres in link frames
+    lsph = [inscribed_spheres(v, K) for v in lverts]
+    # mesh spheres in the world frame (from each mesh's own hull)
+    msph = []
+    for m in range(pack.n):
+        v = pack.verts[pack.vert_off[m]:pack.vert_off[m + 1]]
+        msph.append(inscribed_spheres(v, K))
+    mb = pack.boxes
+    lout = [hull.outer_lod(v, hull.inner_lod(v, hull.OUTER_LOD_K)[1])[0] for v in lverts]
+    lin_pl = [hull.inner_lod(v, hull.INNER_LOD_K)[1] for v in lverts]
+    lfull_pl = [hull.hull_data(v)[1] for v in lverts]
+    min_pl = [pack.inner.planes[pack.inner.plane_off[m]:pack.inner.plane_off[m + 1]] for m in range(pack.n)]
+    mfull_pl = [pack.planes[pack.plane_off[m]:pack.plane_off[m + 1]] for m in range(pack.n)]
+    rem = []
+    mout = [pack.outer.verts[pack.outer.vert_off[m]:pack.outer.vert_off[m + 1]] for m in range(pack.n)]
+    rng = np.random.default_rng(5)
+    stats = dict(pairs=0, coll=0, free=0, sph_coll=0, sph_wrong=0)
+    margins = []
+    t0 = time.time()
+    for it in range(n_cfg):
+        q = LO + (HI - LO) * rng.random(7)
+        fr = O.fk_links(q)
+        for l in range(10):
+            R = fr[l, :9].reshape(3, 3)
+            p = fr[l, 9:]
+            bx = lboxes[l]
+            c_l = R @ bx[:3] + p
+            U = R @ bx[3:12].reshape(3, 3)
+            h_l = bx[12:15]
+            ext_l = np.abs(U) @ h_l
+            for m in range(pack.n):
+                cm, Rm, hm, ihm = mb[m, :3], mb[m, 3:12].reshape(3, 3), mb[m, 12:15], mb[m, 15:18]
+                ext_m = np.abs(Rm) @ hm
+                if np.any(np.abs(c_l - cm) > ext_l + ext_m - PEN):
+                    continue
+                if obb_sat(c_l, U, h_l, cm, Rm, hm) < PEN:
+                    continue
+                if obb_sat(c_l, U, bx[15:18], cm, Rm, ihm) >= PEN:
+                    continue
+                d = O.mesh_pair_pd(l, q, m, 1)
+                stats["pairs"] += 1
+                col = d >= PEN
+                stats["coll" if col else "free"] += 1
+                cl = lsph[l][:, :3] @ R.T + p
+                rl = lsph[l][:, 3]
+                cmsp, rm = msph[m][:, :3], msph[m][:, 3]
+                ov = (rl[:, None] + rm[None, :] - np.linalg.norm(cl[:, None] - cmsp[None], axis=2)).max()
+                if ov >= PEN + 1e-4:
+                    stats["sph_coll"] += 1
+                    if not col:
+                        stats["sph_wrong"] += 1
+                # sphere vs hull: balls of one inside the other hull's (inner LOD) facets
+                def svh(cw, r, R_, p_, pl):
+                    cl_ = (cw - p_) @ R_   # into the hull's frame (R_ rows = world from local)
+                    s_ = (pl[:, 3][None, :] - cl_ @ pl[:, :3].T).min(1)
+                    return (r + np.where(s_ >= 0, s_, -np.inf)).max()
+                I3 = np.eye(3); z3 = np.zeros(3)
+                sv_in = max(svh(cmsp, rm, R, p, lin_pl[l]), svh(cl, rl, I3, z3, min_pl[m]))
+                sv_full = max(svh(cmsp, rm, R, p, lfull_pl[l]), svh(cl, rl, I3, z3, mfull_pl[m]))
+                if sv_in >= PEN + 1e-4:
+                    stats["svh_in_coll"] = stats.get("svh_in_coll", 0) + 1
+                if sv_full >= PEN + 1e-4:
+                    stats["svh_full_coll"] = stats.get("svh_full_coll", 0) + 1
+                if max(sv_full, ov) >= PEN + 1e-4 and not col:
+                    stats["svh_wrong"] = stats.get("svh_wrong", 0) + 1
+                Dm = rl[:, None] + rm[None, :] - np.linalg.norm(cl[:, None] - cmsp[None], axis=2)
+                bi, bj = np.unravel_index(np.argmax(Dm), Dm.shape)
+                sv_b = max(svh(cmsp[bj:bj + 1], rm[bj:bj + 1], R, p, lfull_pl[l]),
+                           svh(cl[bi:bi + 1], rl[bi:bi + 1], I3, z3, mfull_pl[m]))
+                sv_bi = max(svh(cmsp[bj:bj + 1], rm[bj:bj + 1], R, p, lin_pl[l]),
+                           svh(cl[bi:bi + 1], rl[bi:bi + 1], I3, z3, min_pl[m]))
+                if sv_b >= PEN + 1e-4:
+                    stats["svh_best_full"] = stats.get("svh_best_full", 0) + 1
+                if sv_bi >= PEN + 1e-4:
+                    stats["svh_best_in"] = stats.get("svh_best_in", 0) + 1
+                # remaining after sphere-sphere + trial axis
+                lw_ = lverts[l] @ R.T + p
+                mv_ = pack.verts[pack.vert_off[m]:pack.vert_off[m + 1]]
+                a_ = cmsp[bj] - cl[bi]; a_ = a_ / np.linalg.norm(a_)
+                fr_ = (lw_ @ a_).max() - (mv_ @ a_).min() < PEN - 1e-4
+                if not (ov >= PEN + 1e-4 or fr_ or sv_bi >= PEN + 1e-4):
+                    rem.append((col, ov))
+                if col:
+                    margins.append((d, ov))
+                else:
+                    # free certificates: overlap along candidate axes with exact supports
+                    lw = lverts[l] @ R.T + p
+                    mv = pack.verts[pack.vert_off[m]:pack.vert_off[m + 1]]
+                    D = rl[:, None] + rm[None, :] - np.linalg.norm(cl[:, None] - cmsp[None], axis=2)
+                    i, j = np.unravel_index(np.argmax(D), D.shape)
+                    axes = {"sph": cmsp[j] - cl[i], "cen": mv.mean(0) - lw.mean(0)}
+                    axes["box"] = None
+                    for nm, a in axes.items():
+                        if a is None:
+                            continue
+                        a = a / np.linalg.norm(a)
+                        o = (lw @ a).max() - (mv @ a).min()
+                        if o < PEN - 1e-4:
+                            stats["free_" + nm] = stats.get("free_" + nm, 0) + 1
+                    o1 = (lw @ (axes["sph"] / np.linalg.norm(axes["sph"]))).max() - (mv @ (axes["sph"] / np.linalg.norm(axes["sph"]))).min()
+                    o2 = (lw @ (axes["cen"] / np.linalg.norm(axes["cen"]))).max() - (mv @ (axes["cen"] / np.linalg.norm(axes["cen"]))).min()
+                    if min(o1, o2) < PEN - 1e-4:
+                        stats["free_either"] = stats.get("free_either", 0) + 1
+                    a = axes["sph"] / np.linalg.norm(axes["sph"])
+                    lo_w = lout[l] @ R.T + p
+                    o3 = (lo_w @ a).max() - (mout[m] @ a).min()
+                    if o3 < PEN - 1e-4:
+                        stats["free_sph_lod"] = stats.get("free_sph_lod", 0) + 1
+                    # two more axes: the second-best sphere pair, the mesh-centre direction from the best link sphere
+                    Df = D.copy(); Df[i, j] = -np.inf
+                    i2, j2 = np.unravel_index(np.argmax(Df), Df.shape)
+                    best = min(o1, o2)
+                    for a in (cmsp[j2] - cl[i2], mv.mean(0) - cl[i]):
+                        a = a / np.linalg.norm(a)
+                        best = min(best, (lw @ a).max() - (mv @ a).min())
+                    if best < PEN - 1e-4:
+                        stats["free_4ax"] = stats.get("free_4ax", 0) + 1
+        if (it + 1) % 50 == 0:
+            print(it + 1, stats, "%.0f s" % (time.time() - t0), flush=True)
+    print(stats)
+    r = np.array(rem)
+    print("remaining", len(r), "collide", int(r[:, 0].sum()))
+    for t in (-0.1, -0.05, -0.02, 0.0, 0.02):
+        sel = r[:, 1] > t
+        print("  ov > %.2f: %d pairs, %d collide" % (t, sel.sum(), int(r[sel, 0].sum())))
+    if margins:
+        a = np.array(margins)
+        print("collision pairs: depth median %.3f, best sphere overlap median %.3f" %
+              (np.median(a[:, 0]), np.median(a[:, 1])))
+
+
+if __name__ == "__main__":
+    main()

@@ -24,7 +24,7 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
     "tcmp_synchronize",
-    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_mesh_spheres", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_body", "tcmp_base_pd",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
@@ -106,6 +106,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_set_meshes.argtypes = [vp, _dp, _i32p, _dp, _i32p, _i32p, _i32p, _dp, ctypes.c_int32]
         L.tcmp_set_mesh_lods.argtypes = [vp, ctypes.POINTER(Hulls), ctypes.POINTER(Hulls),
                                          ctypes.c_int32]
+        if hasattr(L, "tcmp_set_mesh_spheres"):  # absent from A/B builds of older sources
+            L.tcmp_set_mesh_spheres.argtypes = [vp, _dp, ctypes.c_int32, ctypes.c_int32]
         L.tcmp_set_self_collision.argtypes = [vp, ctypes.c_int32]
         L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
@@ -240,6 +242,11 @@ class Engine:
                 hi, ho = hulls(meshes.inner), hulls(meshes.outer)
                 self._check(self.L.tcmp_set_mesh_lods(self.h, ctypes.byref(hi), ctypes.byref(ho),
                                                       int(len(meshes))))
+            sph = getattr(meshes, "spheres", None)
+            if sph is not None and hasattr(self.L, "tcmp_set_mesh_spheres"):
+                sph = np.ascontiguousarray(sph, dtype=np.float64)
+                self._check(self.L.tcmp_set_mesh_spheres(self.h, _d(sph), int(len(meshes)),
+                                                         int(sph.shape[1])))
         self._mesh_key = mkey
         self._scene_key = key
         self._n_scene = len(obb) + (len(meshes) if meshes is not None else 0)

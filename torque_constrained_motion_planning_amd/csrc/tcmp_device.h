@@ -19,6 +19,7 @@
 #define TCMP_GEO_QUAL static constexpr
 #include "panda_geometry.inc"
 #include "panda_lod.inc"
+#include "panda_spheres.inc"
 
 namespace tcmp {
 
@@ -116,6 +117,9 @@ struct Scene {
   // difference of nearby vertices would lose the direction of short edges)
   const float4* lodev[2];
   const float4* geo_ev;
+  // inscribed spheres [(10 + meshes) * TCMP_NSPH]: the links' (link frames), then each mesh's
+  // (mrange flag 19), the lane-parallel certificates of phase B (sphere_cert)
+  const float4* sph;
   // self-collision pairs (tcmp_set_self_collision): the 10 link hulls are appended to the
   // mesh arrays as meshes n_mesh + j in their own link frames, and their outer-box records
   // follow the obstacles (obs rows n_obs + j, not in tier 0's obstacle loop)
@@ -1156,6 +1160,67 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
     aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
 }
 
+// Lane-parallel certificates for one pending (link, mesh) pair of phase B, ahead of the
+// wave-cooperative exact chain (exact_pair), which handles one pair at a time with the whole
+// wave.  Inscribed spheres of both hulls (Scene::sph, spheres.py / panda_spheres.inc): a sphere
+// pair overlapping by >= kPen + guard proves "collision" (penetration depth is monotone under
+// inclusion, utils.py:2833's -0.04 threshold).  The direction between the most-overlapping
+// pair's centres is then a trial axis: the full hulls' projections on it overlapping by less
+// than kPen - guard prove "free" (the depth is the minimum projection overlap over all
+// directions).  fp32 throughout; its error (a few 1e-7 m for coordinates of a few metres) is
+// far inside the 1e-4 guard, so the decision is the exact test's.  Returns 0 free,
+// 1 collision, 2 undecided.  Mesh m: rows TCMP_NSPH * (10 + m) of sph, world frame (link
+// meshes of self pairs: their own link frame, as the pose is then).
+__device__ __forceinline__ int sphere_cert(int link, const double Rd[9], const double pd[3], int mi,
+                                           const Scene sc, const Geo g) {
+  float R[9], p[3];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = (float)Rd[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = (float)pd[k];
+  const float4* LS = sc.sph + TCMP_NSPH * link;
+  const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);
+  float best = -INFINITY, ax = 1.f, ay = 0.f, az = 0.f;
+  for (int i = 0; i < TCMP_NSPH; ++i) {
+    const float4 s = LS[i];
+    const float cx = R[0] * s.x + R[1] * s.y + R[2] * s.z + p[0];
+    const float cy = R[3] * s.x + R[4] * s.y + R[5] * s.z + p[1];
+    const float cz = R[6] * s.x + R[7] * s.y + R[8] * s.z + p[2];
+#pragma unroll 4
+    for (int j = 0; j < TCMP_NSPH; ++j) {
+      const float4 t = MS[j];
+      const float dx = t.x - cx, dy = t.y - cy, dz = t.z - cz;
+      const float ov = s.w + t.w - __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
+      if (ov > best) { best = ov; ax = dx; ay = dy; az = dz; }
+    }
+  }
+  if (best >= (float)kPen + kExactGuard) return 1;
+  const float l2 = ax * ax + ay * ay + az * az;
+  if (!(l2 > 1e-12f)) return 2;
+  const float il = rsqrtf(l2);
+  ax *= il; ay *= il; az *= il;
+  // link support along a: max over the link-frame vertices of v . (R^T a), plus p . a
+  const float bx = R[0] * ax + R[3] * ay + R[6] * az;
+  const float by = R[1] * ax + R[4] * ay + R[7] * az;
+  const float bz = R[2] * ax + R[5] * ay + R[8] * az;
+  float hl = -INFINITY;
+  const int v1 = tcmp_geo_vert_off[link + 1];
+#pragma unroll 4
+  for (int v = tcmp_geo_vert_off[link]; v < v1; ++v)
+    hl = fmaxf(hl, g.verts32[3 * v] * bx + g.verts32[3 * v + 1] * by + g.verts32[3 * v + 2] * bz);
+  hl += p[0] * ax + p[1] * ay + p[2] * az;
+  // mesh: min over its vertices of w . a
+  const int* rg = sc.mrange + kMrange * mi;
+  const int w1 = rg[1];
+  float hm = INFINITY;
+#pragma unroll 4
+  for (int w = rg[0]; w < w1; ++w) {
+    const float4 x = sc.mv32[w];
+    hm = fminf(hm, x.x * ax + x.y * ay + x.z * az);
+  }
+  return (hl - hm < (float)kPen - kExactGuard) ? 0 : 2;
+}
+
 // MESH = false: a scene without convex meshes (tcmp_set_meshes count 0) -- the mesh tiers
 // are compiled out, which keeps the box-only kernels' register allocation unchanged.
 // The joint-limit test (inclusive, utils.py:3181-3182) is the caller's: `active` lanes are
@@ -1225,13 +1290,23 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #pragma unroll
         for (int k = 0; k < 3; ++k) p[k] = pr[k];
       }
-      int cls = 0;
+      int cls = 0, mi = -1;
       if (has) {
         double wc[3], U[9], aabb[3];
         link_obb(lk, R, p, wc, U, aabb);
         const double* ob = sc.obs + 16 * orow;
-        const int mi = MESH ? obs_mesh(ob) : -1;
+        mi = MESH ? obs_mesh(ob) : -1;
         cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, st);
+      }
+      if (MESH) {
+        // lane-parallel sphere certificates before the wave-serial exact chain
+        const bool sp = cls == 2 && mi >= 0 && sc.mrange[kMrange * mi + 19] != 0;
+        if (__ballot(sp) && sp) {
+          cls = sphere_cert(lk, R, p, mi, sc, g);
+#ifdef TCMP_PROF_EXACT
+          if (cls != 2) atomicAdd(&g_exact_stats[cls ? 14 : 15], 1ull);
+#endif
+        }
       }
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);

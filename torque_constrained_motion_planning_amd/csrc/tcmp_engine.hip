@@ -1033,6 +1033,12 @@ struct tcmp_handle {
   DBuf<float> lodv3[2], lodpl[2];             // link LOD hulls (panda_lod.inc), link frames
   DBuf<unsigned short> lodei[2];
   DBuf<float> lodev[2], geo_ev;               // link hull edge vectors (fp64 -> fp32)
+  // inscribed spheres (certificates): rows [0, 10 * TCMP_NSPH) the links' (panda_spheres.inc,
+  // link frames), then TCMP_NSPH per mesh (tcmp_set_mesh_spheres; link meshes: the links' own)
+  bool user_sph = false;
+  bool use_sph = true;  // TCMP_SPHERES=0 turns the certificate off (A/B)
+  std::vector<double> sph_h;
+  DBuf<float> sph;
   DevState* st = nullptr;
   // plan: parameters on the host and their device copies (kernels read dP, so a captured
   // round graph replays for any query of the same shape); dPx for the standalone entry points
@@ -1129,6 +1135,7 @@ struct tcmp_handle {
       s.lodev[i] = reinterpret_cast<const float4*>(lodev[i].p);
     }
     s.geo_ev = reinterpret_cast<const float4*>(geo_ev.p);
+    s.sph = reinterpret_cast<const float4*>(sph.p);
     s.n_mesh = n_mesh;
     s.self_coll = self_coll;
     return s;
@@ -1620,6 +1627,7 @@ int tcmp_create(int device, tcmp_handle** out) {
   HIPCHK(hipMemset(h->st_nn, 0, sizeof(DevState)));
   if (const char* e = getenv("TCMP_NN_WAVES_PER_CU")) h->nn_waves_per_cu = std::max(1, atoi(e));
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
+  if (const char* e = getenv("TCMP_SPHERES")) h->use_sph = atoi(e) != 0;
   if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(16, std::max(8, atoi(e)));
   if (const char* e = getenv("TCMP_EDGE_SPLIT")) h->edge_split = std::max(1, std::min(4, atoi(e)));
   if (const char* e = getenv("TCMP_NN_CSORT")) h->nn_cand_count_bits = std::min(16, std::max(0, atoi(e)));
@@ -1635,6 +1643,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->planes32.release();
   h->eidx.release();
   h->geo_ev.release();
+  h->sph.release();
   h->obs32.release();
   h->mrange.release();
   for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64, &h->base_geo, &h->base_pd}) b->release();
@@ -1739,6 +1748,7 @@ int check_hulls(const tcmp_hulls* H, int n, const char* what) {
 }
 
 int upload_lods(tcmp_handle* h);
+int upload_spheres(tcmp_handle* h);
 
 // Device mesh arrays from the host copies: the user meshes, then (self-collision on) the 10
 // link hulls in their own link frames as meshes n_mesh + j; then their LOD rows.
@@ -1809,7 +1819,38 @@ int upload_meshes(tcmp_handle* h) {
   HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->mrange_h = rg;
-  return upload_lods(h);
+  if (int rc = upload_lods(h)) return rc;
+  return upload_spheres(h);
+}
+
+// Inscribed spheres (mrange flag 19): the links' rows first, then the user meshes'
+// (tcmp_set_mesh_spheres, world frame) and, self-collision on, the links' own for the link
+// meshes n_mesh + j (link frames).
+int upload_spheres(tcmp_handle* h) {
+  const int n_user = h->n_mesh, n_self = h->self_coll ? TCMP_NLINKS : 0, nm = n_user + n_self;
+  if (nm == 0) return 0;
+  constexpr int K = TCMP_NSPH;
+  std::vector<float> a((size_t)(TCMP_NLINKS + nm) * K * 4, 0.f);
+  for (int i = 0; i < TCMP_NLINKS * K * 4; ++i) a[i] = (float)tcmp_link_spheres[i];
+  std::vector<int> rg = h->mrange_h;
+  for (int m = 0; m < nm; ++m) {
+    const double* src = nullptr;
+    if (m < n_user) {
+      if (h->user_sph) src = h->sph_h.data() + (size_t)m * K * 4;
+    } else {
+      src = tcmp_link_spheres + (size_t)(m - n_user) * K * 4;
+    }
+    rg[kMrange * m + 19] = (src && h->use_sph) ? 1 : 0;
+    if (src)
+      for (int i = 0; i < K * 4; ++i) a[(size_t)(TCMP_NLINKS + m) * K * 4 + i] = (float)src[i];
+  }
+  int rc = h->sph.ensure(a.size());
+  if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->sph.p, a.data(), a.size() * 4, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  h->mrange_h = rg;
+  return 0;
 }
 
 // Level-of-detail hulls of the meshes (rows 6..17 of mrange, flag 18): the user meshes'
@@ -1997,6 +2038,7 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
   }
   h->n_mesh = n_mesh;
   h->user_lods = false;  // new meshes: their LODs come with the next tcmp_set_mesh_lods
+  h->user_sph = false;   // and their spheres with the next tcmp_set_mesh_spheres
   if (int rc = upload_meshes(h)) return rc;
   return upload_scene(h);
 }
@@ -2020,6 +2062,23 @@ int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls
   }
   h->user_lods = true;
   return upload_lods(h);
+}
+
+int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh, int32_t k) {
+  if (int rc = set_dev(h)) return rc;
+  if (n_mesh != h->n_mesh) return fail(-1, "sphere count differs from the mesh count");
+  if (k != TCMP_NSPH) return fail(-1, "spheres per mesh must be " + std::to_string(TCMP_NSPH));
+  if (n_mesh == 0) return 0;
+  if (!spheres) return fail(-1, "null sphere array");
+  for (int i = 0; i < n_mesh * k; ++i) {
+    const double* s = spheres + 4 * (size_t)i;
+    if (!(s[3] >= 0.0) || !std::isfinite(s[0]) || !std::isfinite(s[1]) || !std::isfinite(s[2]) ||
+        !std::isfinite(s[3]))
+      return fail(-1, "bad sphere row " + std::to_string(i));
+  }
+  h->sph_h.assign(spheres, spheres + (size_t)n_mesh * k * 4);
+  h->user_sph = true;
+  return upload_spheres(h);
 }
 
 int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {

@@ -151,6 +151,7 @@ class ConvexMesh:
         self.scale = float(scale)
         self.name = name
         self._rec = None
+        self._sph = None
 
     def world_vertices(self):
         return (self.vertices * self.scale) @ self.rotation.T + self.position
@@ -166,6 +167,14 @@ class ConvexMesh:
             outer = outer_lod(v, inner_lod(v, OUTER_LOD_K)[1])
             self._rec = (v, pl, e, box, inner, outer)
         return self._rec
+
+    def spheres(self):
+        """[spheres.N_SPHERES, 4] balls inside the hull (world frame); cached.  The kernels'
+        lane-parallel certificate ahead of the exact test (tcmp_set_mesh_spheres)."""
+        if self._sph is None:
+            from .spheres import inscribed_spheres
+            self._sph = inscribed_spheres(self.record()[0])
+        return self._sph
 
     def __repr__(self):
         return "ConvexMesh(%s, %d verts, scale %.3g)" % (self.name, len(self.vertices), self.scale)
@@ -198,6 +207,9 @@ class MeshPack(HullSet):
         self.boxes = np.ascontiguousarray(np.array([r[3] for r in recs]).reshape(-1, 18))
         self.inner = HullSet([r[4] for r in recs])
         self.outer = HullSet([r[5] for r in recs])
+        from .spheres import N_SPHERES
+        self.spheres = np.ascontiguousarray(
+            np.array([m.spheres() for m in meshes]).reshape(-1, N_SPHERES, 4))
 
     def key(self):
         return b"".join(a.tobytes() for a in self.arrays() + (self.boxes,) + self.inner.arrays()
