@@ -150,6 +150,23 @@ def main():
                 fr_ = (lw_ @ a_).max() - (mv_ @ a_).min() < PEN - 1e-4
                 if not (ov >= PEN + 1e-4 or fr_ or sv_bi >= PEN + 1e-4):
                     rem.append((col, ov))
+                    if not col:
+                        # facet axes most aligned with the trial axis a_ (from the link to the mesh)
+                        mpl = mfull_pl[m]
+                        lpl = lfull_pl[l]
+                        nl_w = lpl[:, :3] @ R.T
+                        dl_w = lpl[:, 3] + nl_w @ p
+                        got = {}
+                        for kk in (1, 2, 4):
+                            jb = np.argsort(mpl[:, :3] @ a_)[:kk]       # mesh normals ~ -a
+                            ja = np.argsort(-(nl_w @ a_))[:kk]          # link normals ~ +a
+                            best = np.inf
+                            for j in jb:  # u = -n_B: overlap = max_A(-n_B.x) + d_B
+                                best = min(best, (lw_ @ -mpl[j, :3]).max() + mpl[j, 3])
+                            for j in ja:  # u = n_A: overlap = d_A - min_B(n_A.y)
+                                best = min(best, dl_w[j] - (mv_ @ nl_w[j]).min())
+                            if best < PEN - 1e-4:
+                                stats["rem_free_facet%d" % kk] = stats.get("rem_free_facet%d" % kk, 0) + 1
                 if col:
                     margins.append((d, ov))
                 else:

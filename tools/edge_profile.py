@@ -22,7 +22,7 @@ def main():
     prev = [0] * 4
     for q in range(n):
         r, _ = bench.run_query(eng, obs, goal, 1_000_000, 262144, 1234 + q)
-        c = eng.debug_counters(12)
+        c = eng.debug_counters(36)
         ex = [a - b for a, b in zip(c[8:12], prev)]
         prev = c[8:12]
         tot = max(1, c[0])
@@ -33,7 +33,8 @@ def main():
                           "exact32_box_exit": ex[0], "exact32_facets_would_exit": ex[1],
                           "exact32_full": ex[2], "exact32_degenerate": ex[3],
                           "edge_steps": r.edge_steps, "pairs_sat": r.pairs_sat,
-                          "pairs_exact": r.pairs_exact}), flush=True)
+                          "pairs_exact": r.pairs_exact, "box_cert_collision": c[33],
+                          "box_cert_free": c[34]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -29,7 +29,7 @@ def main():
                                     "torque": c[3] / tot, "tail": c[4] / tot,
                                     "exact_in_collision": c[5] / tot, "sincos": c[6] / tot,
                                     "tiers123_in_collision": c[7] / tot},
-                      "sphere_cert": {"collision": c[26], "free": c[27]},
+                      "sphere_cert": {"collision": c[26], "free": c[27]}, "facet_wave_free": c[35],
                       "mesh_exact": {"outer_box_free": c[16], "outer_lod_free": c[17],
                                      "inner_collision": c[18], "hull_hull_fp64": c[19]},
                       "hull_hull_exits": {"mesh_facets": c[20], "link_facets": c[21],

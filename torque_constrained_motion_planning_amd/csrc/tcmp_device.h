@@ -20,6 +20,21 @@
 #include "panda_geometry.inc"
 #include "panda_lod.inc"
 #include "panda_spheres.inc"
+// certificate build knobs: the box form of the lane-parallel certificate, the
+// lane-parallel facet trial axes (both measured slower, off) and the wave-cooperative facet
+// trial axes at the head of the mesh chain (on)
+#ifndef TCMP_BOX_CERT
+#define TCMP_BOX_CERT 0
+#endif
+#ifndef TCMP_FACET_AXES
+#define TCMP_FACET_AXES 0
+#endif
+#ifndef TCMP_FACET_WAVE
+#define TCMP_FACET_WAVE 1
+#endif
+#ifndef TCMP_INNER_FIRST
+#define TCMP_INNER_FIRST 1
+#endif
 
 namespace tcmp {
 
@@ -120,6 +135,11 @@ struct Scene {
   // inscribed spheres [(10 + meshes) * TCMP_NSPH]: the links' (link frames), then each mesh's
   // (mrange flag 19), the lane-parallel certificates of phase B (sphere_cert)
   const float4* sph;
+  // the certificates' link data: the link balls (sph rows [0, 10 * TCMP_NSPH)) and the fp32
+  // link vertices [V][3] -- LDS copies in the mesh kernels (stage_lds), else global
+  const float4* csph;
+  const float* cv32;
+  int box_cert;  // the box certificate (box_cert) on (TCMP_SPHERES=0 turns both off)
   // self-collision pairs (tcmp_set_self_collision): the 10 link hulls are appended to the
   // mesh arrays as meshes n_mesh + j in their own link frames, and their outer-box records
   // follow the obstacles (obs rows n_obs + j, not in tier 0's obstacle loop)
@@ -157,9 +177,10 @@ __host__ __device__ constexpr unsigned stage_lds_bytes(int n_obs) {
 // doubles) and the link poses of its pending exact pairs (12 x 64 doubles) in LDS, so that
 // neither stays in registers across the hull-vs-hull tests.
 constexpr unsigned kStashDoubles = 26 * 64;
+constexpr unsigned kCertLdsBytes = 10 * TCMP_NSPH * 16 + TCMP_TOTAL_VERTS * 12;
 __host__ __device__ constexpr unsigned stage_lds_bytes_lean(int n_obs) {
   return (unsigned)(n_obs > 0 ? n_obs : 1) * (8 * sizeof(float)) + 4 * kQwaveBytes +
-         4 * kStashDoubles * sizeof(double);
+         4 * kStashDoubles * sizeof(double) + kCertLdsBytes;
 }
 __device__ __forceinline__ double* wave_stash(unsigned* wq) {
   const unsigned w = threadIdx.x >> 6;
@@ -173,10 +194,18 @@ __device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* l
     float* o32 = reinterpret_cast<float*>(lds);
     unsigned* wq = reinterpret_cast<unsigned*>(o32 + 8 * n) + (threadIdx.x >> 6) * (kQwaveBytes / 4);
     for (int i = threadIdx.x; i < sc.n_obs * 8; i += blockDim.x) o32[i] = sc.obs32[i];
+    // behind the four queues and the four stashes: the link balls and vertices (sphere_cert)
+    float4* cs = reinterpret_cast<float4*>(reinterpret_cast<unsigned char*>(o32 + 8 * n) +
+                                           4 * kQwaveBytes + 4 * kStashDoubles * sizeof(double));
+    float* cv = reinterpret_cast<float*>(cs + 10 * TCMP_NSPH);
+    for (int i = threadIdx.x; i < 10 * TCMP_NSPH; i += blockDim.x) cs[i] = sc.sph[i];
+    for (int i = threadIdx.x; i < 3 * TCMP_TOTAL_VERTS; i += blockDim.x) cv[i] = g.verts32[i];
     __syncthreads();
     so = sc;
     so.obs32 = o32;
     so.wq = wq;
+    so.csph = cs;
+    so.cv32 = cv;
     go = g;
     return;
   }
@@ -198,6 +227,8 @@ __device__ __forceinline__ void stage_lds(const Scene sc, const Geo g, double* l
   so.obs = o64;
   so.obs32 = o32;
   so.wq = wq;
+  so.csph = sc.sph;
+  so.cv32 = vt;
   go = g;
   go.planes32 = pl;
   go.verts32 = vt;
@@ -823,6 +854,86 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
 #include "tcmp_mesh.h"
 namespace tcmp {
 
+// Wave-cooperative facet trial axes, the first stage of the mesh chain (exact_pair): the pairs
+// that reach it are those the lane-parallel certificates (sphere_cert) left open, and on those
+// the exact test's minimising axis is mostly a facet normal of one hull (tools/cert_study.py).
+// The most-overlapping ball pair (256 pairs, four per lane, wave argmax) gives the direction
+// b (link frame) / a = R b (world); the mesh facet whose outward normal is closest to -a and
+// the link facet whose normal is closest to b (wave argmax each) are tested with the full
+// hulls' supports (link vertices from LDS, mesh vertices from global).  Returns the smaller
+// of the two overlaps -- an upper bound of the depth ("free" below kPen - guard).
+__device__ __forceinline__ float facet_axes_wave(int link, const float R[9], const float p[3], int mi,
+                                                 const int* rg, const Scene sc, const Geo g) {
+  const int lane = lane_id();
+  const float4* LS = sc.csph + TCMP_NSPH * link;
+  const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);
+  float best = -INFINITY, bx = 1.f, by = 0.f, bz = 0.f;
+#pragma unroll
+  for (int k = lane; k < TCMP_NSPH * TCMP_NSPH; k += 64) {
+    const float4 t = MS[k % TCMP_NSPH];
+    const float4 s = LS[k / TCMP_NSPH];
+    const float dx = t.x - p[0], dy = t.y - p[1], dz = t.z - p[2];
+    const float ex = R[0] * dx + R[3] * dy + R[6] * dz - s.x;
+    const float ey = R[1] * dx + R[4] * dy + R[7] * dz - s.y;
+    const float ez = R[2] * dx + R[5] * dy + R[8] * dz - s.z;
+    const float ov = s.w + t.w - __builtin_sqrtf(ex * ex + ey * ey + ez * ez);
+    if (ov > best) { best = ov; bx = ex; by = ey; bz = ez; }
+  }
+  {
+    const float m = wave_maxf(best);
+    const int L = __builtin_ctzll(__ballot(best == m));
+    bx = __shfl(bx, L); by = __shfl(by, L); bz = __shfl(bz, L);
+    const float l2 = bx * bx + by * by + bz * bz;
+    if (!(l2 > 1e-12f)) return INFINITY;
+    const float il = rsqrtf(l2);
+    bx *= il; by *= il; bz *= il;
+  }
+  const float ax = R[0] * bx + R[1] * by + R[2] * bz;
+  const float ay = R[3] * bx + R[4] * by + R[5] * bz;
+  const float az = R[6] * bx + R[7] * by + R[8] * bz;
+  int fm = rg[2], fl = tcmp_geo_plane_off[link];
+  {
+    float sm = -INFINITY, sl = -INFINITY;
+    const int m1 = rg[3];
+    for (int f = rg[2] + lane; f < m1; f += 64) {
+      const float4 n = sc.mp32[f];
+      const float v = -(n.x * ax + n.y * ay + n.z * az);
+      if (v > sm) { sm = v; fm = f; }
+    }
+    const int l1 = tcmp_geo_plane_off[link + 1];
+    for (int f = fl + lane; f < l1; f += 64) {
+      const float4 n = g.planes32[f];
+      const float v = n.x * bx + n.y * by + n.z * bz;
+      if (v > sl) { sl = v; fl = f; }
+    }
+    const float mm = wave_maxf(sm), ml = wave_maxf(sl);
+    fm = __builtin_amdgcn_readfirstlane(__shfl(fm, __builtin_ctzll(__ballot(sm == mm))));
+    fl = __builtin_amdgcn_readfirstlane(__shfl(fl, __builtin_ctzll(__ballot(sl == ml))));
+  }
+  const float4 N = sc.mp32[fm];
+  const float4 F = g.planes32[fl];
+  const float qx = -(R[0] * N.x + R[3] * N.y + R[6] * N.z);  // -n in the link frame
+  const float qy = -(R[1] * N.x + R[4] * N.y + R[7] * N.z);
+  const float qz = -(R[2] * N.x + R[5] * N.y + R[8] * N.z);
+  const float wx = R[0] * F.x + R[1] * F.y + R[2] * F.z;     // the link facet's world normal
+  const float wy = R[3] * F.x + R[4] * F.y + R[5] * F.z;
+  const float wz = R[6] * F.x + R[7] * F.y + R[8] * F.z;
+  float h = -INFINITY, gm = INFINITY;
+  const int v1 = tcmp_geo_vert_off[link + 1];
+  for (int v = tcmp_geo_vert_off[link] + lane; v < v1; v += 64)
+    h = fmaxf(h, sc.cv32[3 * v] * qx + sc.cv32[3 * v + 1] * qy + sc.cv32[3 * v + 2] * qz);
+  const int w1 = rg[1];
+  for (int w = rg[0] + lane; w < w1; w += 64) {
+    const float4 x = sc.mv32[w];
+    gm = fminf(gm, x.x * wx + x.y * wy + x.z * wz);
+  }
+  h = wave_maxf(h);
+  gm = wave_minf(gm);
+  const float o1 = h - (p[0] * N.x + p[1] * N.y + p[2] * N.z) + N.w;
+  const float o2 = F.w + (p[0] * wx + p[1] * wy + p[2] * wz) - gm;
+  return fminf(o1, o2);
+}
+
 // Exact penetration depth of one (link, obstacle) pair, wave-cooperative (all lanes, same
 // arguments); only its comparison with kPen is used.  Boxes: the hull-vs-box test.  Meshes:
 // the link hull against the mesh's outer box ("free" below kPen - guard, the mesh lies inside
@@ -874,9 +985,18 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
-  const float po = exact_pd_wave32(link, pose(), ob, g);
-  TCMP_MESH_CLK(0);
-  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
+  if (TCMP_FACET_WAVE && rg[19]) {
+    float Rf[9], pf[3];
+    {
+      const Pose PL = pose();
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Rf[k] = (float)PL.R[k];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) pf[k] = (float)PL.p[k];
+    }
+    const float fa = facet_axes_wave(link, Rf, pf, mi, rg, sc, g);
+    if (fa < P - kExactGuard) { TCMP_MESH_STAT(23); return (double)fa; }
+  }
   float R[9], p[3];
   {
     const Pose PL = pose();
@@ -885,9 +1005,29 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 #pragma unroll
     for (int k = 0; k < 3; ++k) p[k] = (float)PL.p[k];
   }
+  // level-of-detail certificates: outer LODs contain the hulls ("free" below kPen - guard),
+  // inner LODs lie inside them ("collision" above kPen + guard).  The pairs the lane-parallel
+  // certificates leave open collide far more often than the rest, and a failing "free" test
+  // runs to completion (every axis) while a failing "collision" test exits at its first axis
+  // below the threshold: so, with the certificates on, the inner LODs go first.
+  const bool inner_first = TCMP_INNER_FIRST && rg[18] && rg[19];
+  auto inner_lod = [&]() -> float {
+    const HullA32 Ai{sc.lodv3[0], sc.lodpl[0], sc.lodei[0], sc.lodev[0], tcmp_lod_in_vert_off[link],
+                     tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
+                     tcmp_lod_in_plane_off[link + 1], tcmp_lod_in_edge_off[link],
+                     tcmp_lod_in_edge_off[link + 1]};
+    const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11]};
+    return hull_hull_wave32<false>(Ai, Bi, R, p, P + kExactGuard);
+  };
+  if (inner_first) {
+    const float pi = inner_lod();
+    TCMP_MESH_CLK(2);
+    if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+  }
+  const float po = exact_pd_wave32(link, pose(), ob, g);
+  TCMP_MESH_CLK(0);
+  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
   if (rg[18]) {
-    // level-of-detail certificates: outer LODs contain the hulls ("free" below kPen - guard),
-    // inner LODs lie inside them ("collision" above kPen + guard)
     const HullA32 Ao{sc.lodv3[1], sc.lodpl[1], sc.lodei[1], sc.lodev[1], tcmp_lod_out_vert_off[link],
                      tcmp_lod_out_vert_off[link + 1], tcmp_lod_out_plane_off[link],
                      tcmp_lod_out_plane_off[link + 1], tcmp_lod_out_edge_off[link],
@@ -896,14 +1036,11 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     const float pl = hull_hull_wave32<false>(Ao, Bo, R, p, P - kExactGuard);
     TCMP_MESH_CLK(1);
     if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); return (double)pl; }
-    const HullA32 Ai{sc.lodv3[0], sc.lodpl[0], sc.lodei[0], sc.lodev[0], tcmp_lod_in_vert_off[link],
-                     tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
-                     tcmp_lod_in_plane_off[link + 1], tcmp_lod_in_edge_off[link],
-                     tcmp_lod_in_edge_off[link + 1]};
-    const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11]};
-    const float pi = hull_hull_wave32<false>(Ai, Bi, R, p, P + kExactGuard);
-    TCMP_MESH_CLK(2);
-    if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+    if (!inner_first) {
+      const float pi = inner_lod();
+      TCMP_MESH_CLK(2);
+      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+    }
   } else {
     const double* ib = sc.mib + 16 * mi;
     if (ib[12] > 0.0) {
@@ -1160,6 +1297,9 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
     aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
 }
 
+#ifndef TCMP_CERT_INLINE
+#define TCMP_CERT_INLINE __forceinline__
+#endif
 // Lane-parallel certificates for one pending (link, mesh) pair of phase B, ahead of the
 // wave-cooperative exact chain (exact_pair), which handles one pair at a time with the whole
 // wave.  Inscribed spheres of both hulls (Scene::sph, spheres.py / panda_spheres.inc): a sphere
@@ -1171,54 +1311,228 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 // far inside the 1e-4 guard, so the decision is the exact test's.  Returns 0 free,
 // 1 collision, 2 undecided.  Mesh m: rows TCMP_NSPH * (10 + m) of sph, world frame (link
 // meshes of self pairs: their own link frame, as the pose is then).
-__device__ __forceinline__ int sphere_cert(int link, const double Rd[9], const double pd[3], int mi,
-                                           const Scene sc, const Geo g) {
+__device__ TCMP_CERT_INLINE int sphere_cert(int link, const double Rd[9], const double pd[3], int mi,
+                                            const Scene sc, const Geo g) {
   float R[9], p[3];
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = (float)Rd[k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) p[k] = (float)pd[k];
-  const float4* LS = sc.sph + TCMP_NSPH * link;
-  const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);
+  const float4* LS = sc.csph + TCMP_NSPH * link;               // LDS (mesh kernels)
+  const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);  // global
+  // every mesh ball into the link frame once (u = R^T (t - p)), against the link's balls;
+  // best: the largest overlap r_i + r_j - |u_j - s_i|, its link-frame direction s_i -> u_j
   float best = -INFINITY, ax = 1.f, ay = 0.f, az = 0.f;
-  for (int i = 0; i < TCMP_NSPH; ++i) {
-    const float4 s = LS[i];
-    const float cx = R[0] * s.x + R[1] * s.y + R[2] * s.z + p[0];
-    const float cy = R[3] * s.x + R[4] * s.y + R[5] * s.z + p[1];
-    const float cz = R[6] * s.x + R[7] * s.y + R[8] * s.z + p[2];
+  int bi = 0, bj = 0;
 #pragma unroll 4
-    for (int j = 0; j < TCMP_NSPH; ++j) {
-      const float4 t = MS[j];
-      const float dx = t.x - cx, dy = t.y - cy, dz = t.z - cz;
-      const float ov = s.w + t.w - __builtin_sqrtf(dx * dx + dy * dy + dz * dz);
-      if (ov > best) { best = ov; ax = dx; ay = dy; az = dz; }
+  for (int j = 0; j < TCMP_NSPH; ++j) {
+    const float4 t = MS[j];
+    const float dx = t.x - p[0], dy = t.y - p[1], dz = t.z - p[2];
+    const float ux = R[0] * dx + R[3] * dy + R[6] * dz;
+    const float uy = R[1] * dx + R[4] * dy + R[7] * dz;
+    const float uz = R[2] * dx + R[5] * dy + R[8] * dz;
+    for (int i = 0; i < TCMP_NSPH; ++i) {
+      const float4 s = LS[i];
+      const float ex = ux - s.x, ey = uy - s.y, ez = uz - s.z;
+      const float ov = s.w + t.w - __builtin_sqrtf(ex * ex + ey * ey + ez * ez);
+      if (ov > best) { best = ov; ax = ex; ay = ey; az = ez; bi = i; bj = j; }
     }
   }
   if (best >= (float)kPen + kExactGuard) return 1;
+  const int* rg = sc.mrange + kMrange * mi;
+  if (rg[18]) {
+    // the best pair's balls against the other body's inner LOD hull (inside the full hull):
+    // a ball whose centre c lies inside a convex polytope penetrates it by exactly
+    // r + min over its facets of (d - n.c), so that value (>= 0 slack) is a lower bound of
+    // the pair's depth
+    float sl = INFINITY, sm = INFINITY;
+    {
+      const float4 t = MS[bj];  // the mesh ball in the link frame
+      const float dx = t.x - p[0], dy = t.y - p[1], dz = t.z - p[2];
+      const float lx = R[0] * dx + R[3] * dy + R[6] * dz;
+      const float ly = R[1] * dx + R[4] * dy + R[7] * dz;
+      const float lz = R[2] * dx + R[5] * dy + R[8] * dz;
+      const int f1 = tcmp_lod_in_plane_off[link + 1];
+#pragma unroll 8
+      for (int f = tcmp_lod_in_plane_off[link]; f < f1; ++f) {
+        const float4 n = sc.lodpl[0][f];
+        sl = fminf(sl, n.w - (n.x * lx + n.y * ly + n.z * lz));
+      }
+      sl = (sl >= 0.f && sl < 1e30f) ? sl + t.w : -INFINITY;
+    }
+    {
+      const float4 s = LS[bi];  // the link ball in the world frame
+      const float cx = R[0] * s.x + R[1] * s.y + R[2] * s.z + p[0];
+      const float cy = R[3] * s.x + R[4] * s.y + R[5] * s.z + p[1];
+      const float cz = R[6] * s.x + R[7] * s.y + R[8] * s.z + p[2];
+      const int f1 = rg[9];
+#pragma unroll 8
+      for (int f = rg[8]; f < f1; ++f) {
+        const float4 n = sc.lp32[0][f];
+        sm = fminf(sm, n.w - (n.x * cx + n.y * cy + n.z * cz));
+      }
+      sm = (sm >= 0.f && sm < 1e30f) ? sm + s.w : -INFINITY;
+    }
+    if (fmaxf(sl, sm) >= (float)kPen + kExactGuard) return 1;
+  }
   const float l2 = ax * ax + ay * ay + az * az;
   if (!(l2 > 1e-12f)) return 2;
   const float il = rsqrtf(l2);
-  ax *= il; ay *= il; az *= il;
-  // link support along a: max over the link-frame vertices of v . (R^T a), plus p . a
-  const float bx = R[0] * ax + R[3] * ay + R[6] * az;
-  const float by = R[1] * ax + R[4] * ay + R[7] * az;
-  const float bz = R[2] * ax + R[5] * ay + R[8] * az;
+  // trial axis: b in the link frame, a = R b in the world
+  const float bx = ax * il, by = ay * il, bz = az * il;
+  ax = R[0] * bx + R[1] * by + R[2] * bz;
+  ay = R[3] * bx + R[4] * by + R[5] * bz;
+  az = R[6] * bx + R[7] * by + R[8] * bz;
+  {
+    // overlap along a: the link's support (its vertices, LDS) minus the mesh's minimum
+    float hl = -INFINITY;
+    const int v1 = tcmp_geo_vert_off[link + 1];
+#pragma unroll 4
+    for (int v = tcmp_geo_vert_off[link]; v < v1; ++v)
+      hl = fmaxf(hl, sc.cv32[3 * v] * bx + sc.cv32[3 * v + 1] * by + sc.cv32[3 * v + 2] * bz);
+    float hm = INFINITY;
+    const int w1 = rg[1];
+#pragma unroll 8
+    for (int w = rg[0]; w < w1; ++w) {
+      const float4 x = sc.mv32[w];
+      hm = fminf(hm, x.x * ax + x.y * ay + x.z * az);
+    }
+    if (hl + (p[0] * ax + p[1] * ay + p[2] * az) - hm < (float)kPen - kExactGuard) return 0;
+  }
+#if TCMP_FACET_AXES
+  // More trial axes: the two mesh facets whose outward normals are closest to -a (axis -n:
+  // overlap = max over the link of -n.x, plus d) and the two link facets whose normals are
+  // closest to +a (axis R n: overlap = d + (R n).p - min over the mesh of (R n).y).  On the
+  // pairs the centre axis leaves open, the minimising axis of the exact test is a facet normal
+  // of one of the hulls in most cases (tools/cert_study.py).
+  int m1 = rg[2], m2 = rg[2], k1 = tcmp_geo_plane_off[link], k2 = k1;
+  {
+    float s1 = -INFINITY, s2 = -INFINITY;
+    const int f1 = rg[3];
+#pragma unroll 8
+    for (int f = rg[2]; f < f1; ++f) {
+      const float4 n = sc.mp32[f];
+      const float sc_ = -(n.x * ax + n.y * ay + n.z * az);
+      if (sc_ > s1) { s2 = s1; m2 = m1; s1 = sc_; m1 = f; } else if (sc_ > s2) { s2 = sc_; m2 = f; }
+    }
+    s1 = -INFINITY; s2 = -INFINITY;
+    const int e1 = tcmp_geo_plane_off[link + 1];
+#pragma unroll 8
+    for (int f = k1; f < e1; ++f) {
+      const float4 n = g.planes32[f];
+      const float sc_ = n.x * bx + n.y * by + n.z * bz;
+      if (sc_ > s1) { s2 = s1; k2 = k1; s1 = sc_; k1 = f; } else if (sc_ > s2) { s2 = sc_; k2 = f; }
+    }
+  }
+  const float4 N1 = sc.mp32[m1], N2 = sc.mp32[m2];
+  const float q1x = -(R[0] * N1.x + R[3] * N1.y + R[6] * N1.z);  // -n in the link frame
+  const float q1y = -(R[1] * N1.x + R[4] * N1.y + R[7] * N1.z);
+  const float q1z = -(R[2] * N1.x + R[5] * N1.y + R[8] * N1.z);
+  const float q2x = -(R[0] * N2.x + R[3] * N2.y + R[6] * N2.z);
+  const float q2y = -(R[1] * N2.x + R[4] * N2.y + R[7] * N2.z);
+  const float q2z = -(R[2] * N2.x + R[5] * N2.y + R[8] * N2.z);
+  float h1 = -INFINITY, h2 = -INFINITY;
+  const int v1 = tcmp_geo_vert_off[link + 1];
+#pragma unroll 4
+  for (int v = tcmp_geo_vert_off[link]; v < v1; ++v) {
+    const float x = sc.cv32[3 * v], y = sc.cv32[3 * v + 1], z = sc.cv32[3 * v + 2];
+    h1 = fmaxf(h1, x * q1x + y * q1y + z * q1z);
+    h2 = fmaxf(h2, x * q2x + y * q2y + z * q2z);
+  }
+  const float o1 = h1 - (p[0] * N1.x + p[1] * N1.y + p[2] * N1.z) + N1.w;
+  const float o2 = h2 - (p[0] * N2.x + p[1] * N2.y + p[2] * N2.z) + N2.w;
+  const float4 L1 = g.planes32[k1], L2 = g.planes32[k2];  // link facet normals in the world
+  const float w1x = R[0] * L1.x + R[1] * L1.y + R[2] * L1.z;
+  const float w1y = R[3] * L1.x + R[4] * L1.y + R[5] * L1.z;
+  const float w1z = R[6] * L1.x + R[7] * L1.y + R[8] * L1.z;
+  const float w2x = R[0] * L2.x + R[1] * L2.y + R[2] * L2.z;
+  const float w2y = R[3] * L2.x + R[4] * L2.y + R[5] * L2.z;
+  const float w2z = R[6] * L2.x + R[7] * L2.y + R[8] * L2.z;
+  float g1 = INFINITY, g2 = INFINITY;
+  const int w1 = rg[1];
+#pragma unroll 8
+  for (int w = rg[0]; w < w1; ++w) {
+    const float4 x = sc.mv32[w];
+    g1 = fminf(g1, x.x * w1x + x.y * w1y + x.z * w1z);
+    g2 = fminf(g2, x.x * w2x + x.y * w2y + x.z * w2z);
+  }
+  const float o3 = L1.w + (p[0] * w1x + p[1] * w1y + p[2] * w1z) - g1;
+  const float o4 = L2.w + (p[0] * w2x + p[1] * w2y + p[2] * w2z) - g2;
+  if (fminf(fminf(o1, o2), fminf(o3, o4)) < (float)kPen - kExactGuard) return 0;
+#endif
+  return 2;
+}
+
+// Lane-parallel certificates for one pending (link, box) pair of phase B, the box form of
+// sphere_cert.  For each of the link's inscribed balls: its centre in the box frame x, the
+// inside slack min_k (h_k - |x_k|) and, outside, the distance to the box.  A ball whose centre
+// lies inside the box penetrates it by exactly r + slack, a lower bound of the pair's depth
+// ("collision" at kPen + guard and above).  Otherwise the most-overlapping ball's direction to
+// its closest box point (inside: its nearest face's inward normal) is a trial axis: the link
+// hull's support (its vertices) and the box's exact support overlapping by less than
+// kPen - guard prove "free".  fp32, errors far inside the 1e-4 guard.  0 free, 1 collision,
+// 2 undecided.  ob: c(3), B(9, row-major, columns = axes), h(3).
+__device__ TCMP_CERT_INLINE int box_cert(int link, const double Rd[9], const double pd[3],
+                                         const double* ob, const Scene sc, const Geo g) {
+  // everything in the box frame: x = M s + t with M = B^T R, t = B^T (p - c) (fp64, then fp32)
+  float M[9], t[3], h[3];
+  {
+    const double d0 = pd[0] - ob[0], d1 = pd[1] - ob[1], d2 = pd[2] - ob[2];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const double b0 = ob[3 + i], b1 = ob[6 + i], b2 = ob[9 + i];
+#pragma unroll
+      for (int j = 0; j < 3; ++j) M[3 * i + j] = (float)(b0 * Rd[j] + b1 * Rd[3 + j] + b2 * Rd[6 + j]);
+      t[i] = (float)(b0 * d0 + b1 * d1 + b2 * d2);
+      h[i] = (float)ob[12 + i];
+    }
+  }
+  const float4* LS = sc.sph + TCMP_NSPH * link;
+  float best = -INFINITY, bx0 = 0.f, bx1 = 0.f, bx2 = 0.f, bs = 0.f;
+  for (int i = 0; i < TCMP_NSPH; ++i) {
+    const float4 s = LS[i];
+    const float x0 = M[0] * s.x + M[1] * s.y + M[2] * s.z + t[0];
+    const float x1 = M[3] * s.x + M[4] * s.y + M[5] * s.z + t[1];
+    const float x2 = M[6] * s.x + M[7] * s.y + M[8] * s.z + t[2];
+    const float e0 = fabsf(x0) - h[0], e1 = fabsf(x1) - h[1], e2 = fabsf(x2) - h[2];
+    const float slack = -fmaxf(e0, fmaxf(e1, e2));
+    const float o0 = fmaxf(e0, 0.f), o1 = fmaxf(e1, 0.f), o2 = fmaxf(e2, 0.f);
+    const float v = slack >= 0.f ? s.w + slack : s.w - __builtin_sqrtf(o0 * o0 + o1 * o1 + o2 * o2);
+    if (v > best) { best = v; bx0 = x0; bx1 = x1; bx2 = x2; bs = slack; }
+  }
+  if (bs >= 0.f && best >= (float)kPen + kExactGuard) return 1;
+#ifdef TCMP_BALL_ONLY
+  return 2;
+#endif
+  // trial axis a (box frame), from the link into the box
+  float a0, a1, a2;
+  if (bs < 0.f) {
+    a0 = fminf(fmaxf(bx0, -h[0]), h[0]) - bx0;
+    a1 = fminf(fmaxf(bx1, -h[1]), h[1]) - bx1;
+    a2 = fminf(fmaxf(bx2, -h[2]), h[2]) - bx2;
+  } else {
+    const float s0 = h[0] - fabsf(bx0), s1 = h[1] - fabsf(bx1), s2 = h[2] - fabsf(bx2);
+    a0 = (s0 <= s1 && s0 <= s2) ? (bx0 < 0.f ? 1.f : -1.f) : 0.f;
+    a1 = (a0 == 0.f && s1 <= s2) ? (bx1 < 0.f ? 1.f : -1.f) : 0.f;
+    a2 = (a0 == 0.f && a1 == 0.f) ? (bx2 < 0.f ? 1.f : -1.f) : 0.f;
+  }
+  const float l2 = a0 * a0 + a1 * a1 + a2 * a2;
+  if (!(l2 > 1e-12f)) return 2;
+  const float il = rsqrtf(l2);
+  a0 *= il; a1 *= il; a2 *= il;
+  // overlap along a: max_v v.(M^T a) + t.a (the link's support, box frame) minus the box's
+  // support on -a, -(h0 |a0| + h1 |a1| + h2 |a2|)
+  const float lx = M[0] * a0 + M[3] * a1 + M[6] * a2;
+  const float ly = M[1] * a0 + M[4] * a1 + M[7] * a2;
+  const float lz = M[2] * a0 + M[5] * a1 + M[8] * a2;
   float hl = -INFINITY;
   const int v1 = tcmp_geo_vert_off[link + 1];
 #pragma unroll 4
   for (int v = tcmp_geo_vert_off[link]; v < v1; ++v)
-    hl = fmaxf(hl, g.verts32[3 * v] * bx + g.verts32[3 * v + 1] * by + g.verts32[3 * v + 2] * bz);
-  hl += p[0] * ax + p[1] * ay + p[2] * az;
-  // mesh: min over its vertices of w . a
-  const int* rg = sc.mrange + kMrange * mi;
-  const int w1 = rg[1];
-  float hm = INFINITY;
-#pragma unroll 4
-  for (int w = rg[0]; w < w1; ++w) {
-    const float4 x = sc.mv32[w];
-    hm = fminf(hm, x.x * ax + x.y * ay + x.z * az);
-  }
-  return (hl - hm < (float)kPen - kExactGuard) ? 0 : 2;
+    hl = fmaxf(hl, g.verts32[3 * v] * lx + g.verts32[3 * v + 1] * ly + g.verts32[3 * v + 2] * lz);
+  const float ov = hl + t[0] * a0 + t[1] * a1 + t[2] * a2 + h[0] * fabsf(a0) + h[1] * fabsf(a1) +
+                   h[2] * fabsf(a2);
+  return (ov < (float)kPen - kExactGuard) ? 0 : 2;
 }
 
 // MESH = false: a scene without convex meshes (tcmp_set_meshes count 0) -- the mesh tiers
@@ -1297,6 +1611,15 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         const double* ob = sc.obs + 16 * orow;
         mi = MESH ? obs_mesh(ob) : -1;
         cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, st);
+        // boxes: the lane-parallel ball / trial-axis certificate before the wave-serial exact
+        // test -- measured slower on C3 (its registers cost more than the exact tests it
+        // saves), so a build knob, off
+        if (TCMP_BOX_CERT && cls == 2 && mi < 0 && sc.box_cert) {
+          cls = box_cert(lk, R, p, ob, sc, g);
+#ifdef TCMP_PROF_EXACT
+          if (cls != 2) atomicAdd(&g_exact_stats[cls ? 21 : 22], 1ull);
+#endif
+        }
       }
       if (MESH) {
         // lane-parallel sphere certificates before the wave-serial exact chain

@@ -1136,6 +1136,7 @@ struct tcmp_handle {
     }
     s.geo_ev = reinterpret_cast<const float4*>(geo_ev.p);
     s.sph = reinterpret_cast<const float4*>(sph.p);
+    s.box_cert = use_sph ? 1 : 0;
     s.n_mesh = n_mesh;
     s.self_coll = self_coll;
     return s;
@@ -1502,6 +1503,7 @@ PlanParams default_params() {
   return P;
 }
 
+int upload_spheres(tcmp_handle* h);  // (below) the links' and meshes' inscribed spheres
 }  // namespace
 
 // ==========================================================================================
@@ -1609,6 +1611,9 @@ int tcmp_create(int device, tcmp_handle** out) {
       if (rc) { delete h; return rc; }
       HIPCHK(hipMemcpy(h->lodev[i].p, ev.data(), ev.size() * 4, hipMemcpyHostToDevice));
     }
+    // the links' inscribed spheres (box and mesh certificates in phase B)
+    rc = upload_spheres(h);
+    if (rc) { delete h; return rc; }
     // dynamic LDS above 64 KiB per workgroup must be allowed explicitly
     const int lim = (int)stage_lds_bytes(kMaxObstacles);
     for (const void* k : {(const void*)k_edges<false, 1>, (const void*)k_edges<true, 1>,
@@ -1828,7 +1833,6 @@ int upload_meshes(tcmp_handle* h) {
 // meshes n_mesh + j (link frames).
 int upload_spheres(tcmp_handle* h) {
   const int n_user = h->n_mesh, n_self = h->self_coll ? TCMP_NLINKS : 0, nm = n_user + n_self;
-  if (nm == 0) return 0;
   constexpr int K = TCMP_NSPH;
   std::vector<float> a((size_t)(TCMP_NLINKS + nm) * K * 4, 0.f);
   for (int i = 0; i < TCMP_NLINKS * K * 4; ++i) a[i] = (float)tcmp_link_spheres[i];
@@ -1847,7 +1851,8 @@ int upload_spheres(tcmp_handle* h) {
   int rc = h->sph.ensure(a.size());
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(h->sph.p, a.data(), a.size() * 4, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
+  if (nm)
+    HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   h->mrange_h = rg;
   return 0;
