@@ -90,7 +90,8 @@ int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls
                        int32_t n_mesh);
 
 /* Optional inscribed spheres for the current meshes (call after tcmp_set_meshes; cleared by
- * it): spheres[n_mesh][k][4] = (cx, cy, cz, r), world frame, each ball inside mesh m's hull;
+ * it): spheres[n_mesh][k][4] = (cx, cy, cz, r), world frame, each ball inside mesh m's hull
+ * (checked against the stored facet planes, n.c + r <= d + 1e-9; status -1 otherwise);
  * k must be 16.  Like the LODs they are certificates only (same reference semantics,
  * utils.py:2833 closest points at -0.04): a link sphere and a mesh sphere overlapping by
  * >= 0.04 + 1e-4 prove "collision", and the full hulls' projections on the direction between
@@ -197,7 +198,7 @@ typedef struct {
   int64_t n_waypoints;    /* len(goal_n.retrace()) */
   int64_t n_traj;         /* min-jerk samples */
   int64_t first_fail;
-  uint64_t edge_steps;    /* extend steps checked */
+  uint64_t edge_steps;    /* extend steps checked (the new edges', then the rewire edges') */
   uint64_t pairs_tested;  /* link x obstacle pair classifications */
   uint64_t pairs_sat;     /* pairs reaching the OBB SAT tier */
   uint64_t pairs_exact;   /* exact hull tests */
@@ -213,6 +214,8 @@ typedef struct {
   uint64_t snap_sum;      /* sum over rounds of the snapshot size T_r */
   uint64_t nn_full_pairs; /* sum over rounds of T_r * B_r: the brute-force scan's pair count */
   int64_t launches_nn_scan; /* k_nearest_wave32 launches (a one-node first round needs none) */
+  uint64_t n_rewires;     /* new.rewire(n, d, path[:-1]) calls (rrt_star.py:187-192) on this
+                             engine's lanes */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

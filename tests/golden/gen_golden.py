@@ -255,8 +255,38 @@ def boxes_scene(rng, n, avoid):
     return np.array(boxes).reshape(-1, 15)
 
 
+class _NodeLog:
+    """Records the reference's OptimalNode graph (rrt_star.py:18-63) while a run builds it:
+    every node in creation order (= the order of `nodes`, rrt_star.py:185) and every
+    OptimalNode.rewire call (rrt_star.py:47-58), through a subclass swapped in for the
+    module attribute rrt_star_force_aware instantiates."""
+
+    def __init__(self):
+        self.nodes = []
+        self.rewires = 0
+        log = self
+
+        class Node(ref_rrt.OptimalNode):
+            def __init__(self, *a, **kw):
+                super().__init__(*a, **kw)
+                log.nodes.append(self)
+
+            def rewire(self, *a, **kw):
+                log.rewires += 1
+                return super().rewire(*a, **kw)
+        self.cls = Node
+
+    def arrays(self):
+        ix = {id(n): i for i, n in enumerate(self.nodes)}
+        cfg = np.array([np.asarray(n.config, dtype=np.float64) for n in self.nodes])
+        cost = np.array([float(n.cost) for n in self.nodes])
+        par = np.array([-1 if n.parent is None else ix[id(n.parent)] for n in self.nodes],
+                       dtype=np.int32)
+        return cfg, cost, par
+
+
 def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, stride=1,
-                  want_found=None, informed=False):
+                  want_found=None, informed=False, radius=0.01):
     problem = Problem(mass, exec_time, mode)
     torque_fn = TESTS[mode](problem)
     collision_fn = make_collision_fn(obs)
@@ -266,15 +296,18 @@ def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, st
     dynam_fn = make_dynam_fn(problem, wp_rec)
     random.seed(seed)
     np.random.seed(seed)
-    saved = ref_rrt.random
+    saved = ref_rrt.random, ref_rrt.OptimalNode
+    log = _NodeLog()
     ref_rrt.random = rnd
+    ref_rrt.OptimalNode = log.cls
     t0 = time.time()
     try:
+        # the planner passes a one-element list (panda_primitives.py:346)
         path, vels, accels, psg = ref_rrt.rrt_star_force_aware(
             tuple(start), tuple(goal), distance_fn, sample, extend_fn, collision_fn, torque_fn,
-            dynam_fn, radius=[0.01], max_time=50, max_iterations=iters, informed=informed)
+            dynam_fn, radius=[radius], max_time=50, max_iterations=iters, informed=informed)
     finally:
-        ref_rrt.random = saved
+        ref_rrt.random, ref_rrt.OptimalNode = saved
     dt = time.time() - t0
     if want_found is not None and (path is not None) != want_found:
         return False
@@ -285,7 +318,10 @@ def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, st
                replay_random=np.array(rnd.vals, dtype=np.float64),
                replay_uniform=np.array(sample.u, dtype=np.float64).reshape(-1, 7),
                found=np.array(path is not None), stride=np.array(stride),
-               informed=np.array(bool(informed)))
+               informed=np.array(bool(informed)), radius=np.array(float(radius)),
+               n_rewires=np.array(log.rewires))
+    cfg, cost, par = log.arrays()
+    res["tree_cfg"], res["tree_cost"], res["tree_parent"] = cfg, cost, par
     if wp_rec:
         res["waypoints"] = wp_rec[-1]
     if path is not None:
@@ -296,9 +332,10 @@ def run_reference(name, start, goal, obs, mode, mass, exec_time, iters, seed, st
         res["q"] = q[idx]; res["qd"] = qd[idx]; res["qdd"] = qdd[idx]; res["psg"] = p[idx]
         res["sum_q"] = q.sum(0); res["sum_qd"] = qd.sum(0); res["sum_qdd"] = qdd.sum(0)
     np.savez_compressed(os.path.join(HERE, "rrt_%s.npz" % name), **res)
-    print("%-22s found=%s waypoints=%s traj=%s random=%d uniform=%d  %.1fs" % (
+    print("%-22s found=%s waypoints=%s traj=%s random=%d uniform=%d nodes=%d rewires=%d  %.1fs" % (
         name, path is not None, len(wp_rec[-1]) if wp_rec else None,
-        len(path) if path is not None else None, len(rnd.vals), len(sample.u), dt))
+        len(path) if path is not None else None, len(rnd.vals), len(sample.u), len(cfg),
+        log.rewires, dt))
     return True
 
 
@@ -359,7 +396,36 @@ def gen_informed():
                   2 * int(z["iters"]), int(z["seed"]), stride=7, want_found=True, informed=True)
 
 
+def gen_rewire():
+    """Reference runs at the large rewire radii where OptimalNode.rewire actually fires
+    (rrt_star.py:183-192; the planner's radius=[0.01] never rewires: every other golden has
+    n_rewires = 0).  Each fixture stores the reference's final tree (configs, costs, parents
+    in node order) and its rewire count, and must have rewired at least `min_rw` times."""
+    rng = np.random.default_rng(4321)
+    cases = [  # name, obstacles, mode, mass, exec_time, iterations, seed, radius, min_rw
+        ("rewire_empty_rne5_r4", 0, "rne", 5.0, 1.0, 400, 11, 4.0, 1),
+        ("rewire_box4_nov2_r8", 4, "nov", 2.0, 1.0, 300, 12, 8.0, 50),
+        ("rewire_box16_rne5_r6", 16, "rne", 5.0, 1.0, 500, 13, 6.0, 20),
+        ("rewire_box8_base_r8", 8, "base", 0.0, 0.5, 250, 14, 8.0, 50),
+    ]
+    for name, n_obs, mode, mass, et, iters, seed, radius, min_rw in cases:
+        for attempt in range(60):
+            s, g, o = pick_query(rng, n_obs, mode, mass, need_block=True, iters=iters,
+                                 random_start=n_obs == 0)
+            if not run_reference(name, s, g, o, mode, mass, et, iters, seed + 100 * attempt,
+                                 want_found=True, radius=radius):
+                continue
+            z = np.load(os.path.join(HERE, "rrt_%s.npz" % name))
+            if int(z["n_rewires"]) >= min_rw:
+                break
+        else:
+            raise RuntimeError("no rewiring golden query for " + name)
+
+
 def main():
+    if "--only-rewire" in sys.argv:
+        gen_rewire()
+        return
     if "--only-informed" in sys.argv:
         gen_informed()
         return

@@ -96,12 +96,14 @@ def _plan(O, qid):
 def _shard_worker(rank, world, port, n_queries, q):
     """One rank of the shard path: round-robin deal, planning (the oracle stands in for the
     engine), shard.pack_paths, the size all-gather, and rank 0's staging of every rank's
-    contribution at tcmp_gather_layout's offsets (shard.stage_rank0).  gloo only carries the
+    contribution at tcmp_gather_layout's offsets (dist_helpers.stage_rank0).  gloo only carries the
     packed buffers between the processes -- RCCL's ncclSend/ncclRecv on the GPU."""
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import torch
     import torch.distributed as dist
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import dist_helpers
     import oracle as O
     from torque_constrained_motion_planning_amd import shard
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -123,7 +125,7 @@ def _shard_worker(rank, world, port, n_queries, q):
             dist.recv(b, src=r)
             hh = h.numpy().reshape(-1, 2)
             packed.append((hh[:, 0], hh[:, 1], b.numpy().reshape(-1, 22)))
-        got = shard.unpack_paths(*shard.stage_rank0(packed, sizes))
+        got = shard.unpack_paths(*dist_helpers.stage_rank0(packed, sizes))
         q.put((got, shard.gather_ok(got, range(n_queries), sizes)))
     else:
         dist.send(torch.from_numpy(np.stack([ids, rows], 1).reshape(-1).copy()), dst=0)
@@ -137,6 +139,7 @@ def test_gather_layout_and_staging(world):
     """tcmp_gather_layout (rank 0's receive offsets, libtcmp.so) + shard.pack_paths /
     stage_rank0 / unpack_paths at world sizes 2..8, ragged: ranks without queries, queries
     without rows (failed plans), 64 C4 queries dealt round-robin."""
+    import dist_helpers
     from torque_constrained_motion_planning_amd import _lib, shard
     rng = np.random.default_rng(world)
     n_q = 64
@@ -151,7 +154,7 @@ def test_gather_layout_and_staging(world):
     assert tq == sizes[:, 0].sum() and tr == sizes[:, 1].sum()
     assert q_off[0] == 0 and r_off[0] == 0
     assert np.array_equal(np.diff(q_off), sizes[:-1, 0]) and np.array_equal(np.diff(r_off), sizes[:-1, 1])
-    ids, rows, body = shard.stage_rank0(packed, sizes)
+    ids, rows, body = dist_helpers.stage_rank0(packed, sizes)
     assert (ids >= 0).all() and not np.isnan(body).any()  # every slot written exactly
     got = shard.unpack_paths(ids, rows, body)
     expect = [i for r in range(world) if r != 1 for i in shard.queries_for_rank(n_q, world, r)]

@@ -132,3 +132,29 @@ def test_grasp_rejected_by_link0(capsys, depth, rejected):
         assert "Grasp IK failure" in out and "found grasp" not in out
     else:
         assert "Grasp IK failure" not in out and "found grasp" in out
+
+
+@pytest.mark.parametrize("meshes", [False, True])
+def test_check_body_ignores_self_pairs(eng, meshes):
+    """The body check is robot vs obstacles (pairwise_collision(robot, b) for b in obstacles,
+    panda_primitives.py:260): with tcmp_set_self_collision on, a configuration that only
+    self-collides is still free for it, while collision_fn reports it."""
+    from torque_constrained_motion_planning_amd.scene import (Box, mesh_pack, obstacle_array,
+                                                               random_mesh_scene)
+    rng = np.random.default_rng(21)
+    q = LO + (HI - LO) * rng.random((3000, 7))
+    far = [Box(center=(3.0, 3.0, 3.0), size=(0.1, 0.1, 0.1))]
+    pack = mesh_pack(random_mesh_scene(rng, 4, lo=(2.5, 2.5, 2.5), hi=(3.5, 3.5, 3.5))) \
+        if meshes else None
+    eng.set_scene(obstacle_array(far), pack)
+    try:
+        eng.set_self_collision(True)
+        O.set_self_collision(True)
+        self_hit = np.array([O.collision(x, None, cull=2) for x in q])
+        assert self_hit.sum() > 20  # ~4 % of uniform configurations self-collide
+        assert np.array_equal(eng.collides(q), self_hit)
+        assert not eng.collides_body(q).any()
+    finally:
+        eng.set_self_collision(False)
+        O.set_self_collision(False)
+    assert not eng.collides_body(q).any()

@@ -115,11 +115,21 @@ def test_host_loop_reproduces_reference(path):
     torque = _OracleTorque(int(z["mode"]), float(z["mass"]))
     random.seed(int(z["seed"]))
     np.random.seed(int(z["seed"]))
-    p, v, a, psg = RS.rrt_star_force_aware(tuple(z["start"]), tuple(z["goal"]), dist, sample, ext,
-                                           coll, torque, _numpy_dynam_fn(float(z["exec_time"])),
-                                           radius=[0.01], max_time=50,
-                                           max_iterations=int(z["iters"]),
-                                           informed=bool(z["informed"]) if "informed" in z else False)
+    st = {}
+    # rrt_star_force_aware dispatches these (foreign collision / torque) callbacks to the host
+    # loop; it is called directly to read back its tree and rewire count
+    p, v, a, psg = RS._rrt_host(tuple(z["start"]), tuple(z["goal"]), dist, sample, ext,
+                                coll, torque, _numpy_dynam_fn(float(z["exec_time"])),
+                                radius=[float(z["radius"]) if "radius" in z else 0.01],
+                                max_time=50, max_iterations=int(z["iters"]),
+                                informed=bool(z["informed"]) if "informed" in z else False,
+                                stats=st)
+    if "tree_cfg" in z:  # the reference's OptimalNode graph and rewire count (rrt_star.py:183-192)
+        t = st["tree"]
+        assert st["n_rewires"] == int(z["n_rewires"]) > 0
+        assert np.array_equal(t.q[:len(t)], z["tree_cfg"])
+        assert np.array_equal(np.array(t.parent), z["tree_parent"])
+        assert np.abs(np.array(t.cost) - z["tree_cost"]).max() < 1e-12
     assert (p is not None) == bool(z["found"])
     if p is None:
         return

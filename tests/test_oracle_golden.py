@@ -46,9 +46,18 @@ def test_rrt_replay_matches_reference(path):
     z = np.load(path)
     rr = z["replay_random"] if len(z["replay_random"]) else np.zeros(0)
     ru = z["replay_uniform"] if len(z["replay_uniform"]) else np.zeros((0, 7))
+    radius = float(z["radius"]) if "radius" in z else 0.01
     r = O.rrt_run(z["start"], z["goal"], int(z["iters"]), z["obs"], int(z["mode"]),
                   float(z["mass"]), float(z["exec_time"]), replay_random=rr, replay_uniform=ru,
-                  informed=bool(z["informed"]) if "informed" in z else False)
+                  informed=bool(z["informed"]) if "informed" in z else False, radius=radius,
+                  tree="tree_cfg" in z)
+    if "tree_cfg" in z:
+        # the reference's OptimalNode graph, node by node, and its rewire count
+        assert r["n_rewires"] == int(z["n_rewires"])
+        assert r["n_nodes"] == len(z["tree_cfg"])
+        assert np.array_equal(r["tree_cfg"], z["tree_cfg"])
+        assert np.array_equal(r["tree_parent"], z["tree_parent"])
+        assert np.abs(r["tree_cost"] - z["tree_cost"]).max() < 1e-12
     found = bool(z["found"])
     assert (r["status"] == 0) == found
     if not found:

@@ -1,0 +1,60 @@
+#!/bin/bash
+# One gpurun call made of named stages, run in order; the first failing stage ends the call.
+#   bash tools/gpu_job.sh TAG STAGE [STAGE ...]
+# stages:
+#   tests[=K]        pytest -m gpu (optionally -k K), then smoke()
+#   bench[=W]        bench.py line for workload W (c3 default), 5 steps (c5: 2)
+#   trace[=W]        rocprofv3 --kernel-trace --stats of the same bench command
+#   pmc[=W]          PMC passes FETCH_SIZE / WRITE_SIZE (one run each) over one bench step
+#   sq[=W]           PMC pass of SQ wave / busy counters over one bench step
+#   env:VAR=V        export VAR=V for the following stages (A/B knobs, TCMP_LIB_PATH=...)
+# Outputs under gpurun_out/TAG/.
+set -e -o pipefail
+TAG=${1:?tag}; shift
+O=gpurun_out/$TAG; mkdir -p $O
+export TMPDIR=/tmp
+bench_args() {  # workload -> bench.py arguments of one measured line
+  case "$1" in
+    c5) echo "--workload c5 --steps 2 --warmup 1" ;;
+    c3|"") echo "--steps 5 --warmup 1" ;;
+    *) echo "--workload $1 --steps 5 --warmup 1" ;;
+  esac
+}
+for st in "$@"; do
+  name=${st%%=*}; arg=""; [ "$name" != "$st" ] && arg=${st#*=}
+  case "$name" in
+    tests)
+      if [ -n "$arg" ]; then
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread -k "$arg" > $O/gpu_tests.log 2>&1
+      else
+        timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/gpu_tests.log 2>&1
+      fi
+      timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 ;;
+    bench)
+      w=${arg:-c3}
+      timeout -k 10 300 python -u bench.py $(bench_args $w) > $O/bench_$w.json 2> $O/bench_$w.err ;;
+    trace)
+      w=${arg:-c3}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$w -o run --output-format csv \
+        -- python3 bench.py $(bench_args $w) --no-cpu-baseline --no-alt > $O/trace_$w.json 2> $O/trace_$w.err ;;
+    pmc)
+      w=${arg:-c3}; i=0
+      for grp in FETCH_SIZE WRITE_SIZE; do
+        i=$((i+1))
+        timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-trace -d $O/pmc_$w/p$i -o run --output-format csv \
+          -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
+          --no-cpu-baseline --no-alt > $O/pmc_${w}_p$i.log 2>&1
+      done ;;
+    sq)
+      w=${arg:-c3}
+      timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
+        --kernel-trace -d $O/sq_$w -o run --output-format csv \
+        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
+        --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
+    env:*)
+      export "${st#env:}" ;;
+    *) echo "unknown stage $st" >&2; exit 2 ;;
+  esac
+  echo "$st ok" >> $O/STAGES
+done
+echo done > $O/DONE

@@ -72,7 +72,7 @@ class PlanResult(ctypes.Structure):
         ("ms_finish", ctypes.c_double), ("launches_nearest", ctypes.c_int64),
         ("nn_box_tests", ctypes.c_uint64), ("ms_nn_scan", ctypes.c_double),
         ("snap_sum", ctypes.c_uint64), ("nn_full_pairs", ctypes.c_uint64),
-        ("launches_nn_scan", ctypes.c_int64),
+        ("launches_nn_scan", ctypes.c_int64), ("n_rewires", ctypes.c_uint64),
     ]
 
     def as_dict(self):

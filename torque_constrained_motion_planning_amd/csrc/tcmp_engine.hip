@@ -605,6 +605,7 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
   int c = 0;
   int prev = -1;
   unsigned long long rew = 0;
+  unsigned steps = 0;  // extend steps of the rewire edges (counted like k_edges')
   while (true) {
     // next neighbour in index order (stored list, then a serial rescan past the list)
     int nidx = -1;
@@ -653,6 +654,7 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
                                               : torque_ok<false>(cq, sq, z, z, P.mass);
       }
       if (alive) {
+        ++steps;
         if (ok) {
           for (int k = 0; k < 7; ++k) q[k] = qq[k];
           ++i;
@@ -672,8 +674,9 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
       ++rew;
     }
   }
-  const unsigned long long r = wave_sum_u64(rew);
+  const unsigned long long r = wave_sum_u64(rew), sn = wave_sum_u64((unsigned long long)steps);
   if (lane_id() == 0 && r) atomicAdd(&st->rewires, r);
+  if (lane_id() == 0 && sn) atomicAdd(&st->edge_steps, sn);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1634,7 +1637,11 @@ int tcmp_create(int device, tcmp_handle** out) {
   if (const char* e = getenv("TCMP_GRAPHS")) h->use_graphs = atoi(e) != 0;
   if (const char* e = getenv("TCMP_SPHERES")) h->use_sph = atoi(e) != 0;
   if (const char* e = getenv("TCMP_NN_CBITS")) h->nn_cand_bits = std::min(16, std::max(8, atoi(e)));
-  if (const char* e = getenv("TCMP_EDGE_SPLIT")) h->edge_split = std::max(1, std::min(4, atoi(e)));
+  if (const char* e = getenv("TCMP_EDGE_SPLIT")) {
+    // lanes per edge: a power of two (k_edges<., 1|2|4>), rounded down
+    const int v = std::max(1, std::min(4, atoi(e)));
+    h->edge_split = v >= 4 ? 4 : v >= 2 ? 2 : 1;
+  }
   if (const char* e = getenv("TCMP_NN_CSORT")) h->nn_cand_count_bits = std::min(16, std::max(0, atoi(e)));
   *out = h;
   return 0;
@@ -2080,6 +2087,16 @@ int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh,
     if (!(s[3] >= 0.0) || !std::isfinite(s[0]) || !std::isfinite(s[1]) || !std::isfinite(s[2]) ||
         !std::isfinite(s[3]))
       return fail(-1, "bad sphere row " + std::to_string(i));
+    // the certificates are sound only for balls inside the hull: n.c + r <= d on every facet
+    const int m = i / k;
+    double out = -INFINITY;
+    for (int f = h->mesh_poff[m]; f < h->mesh_poff[m + 1]; ++f) {
+      const double* p = h->mesh_p.data() + 4 * (size_t)f;
+      out = std::max(out, p[0] * s[0] + p[1] * s[1] + p[2] * s[2] - p[3]);
+    }
+    if (out + s[3] > 1e-9)
+      return fail(-1, "sphere row " + std::to_string(i) + " is not inside mesh " +
+                          std::to_string(m) + "'s hull");
   }
   h->sph_h.assign(spheres, spheres + (size_t)n_mesh * k * 4);
   h->user_sph = true;
@@ -2244,9 +2261,15 @@ int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collide
   rc = rc ? rc : h->i0.ensure((size_t)n);
   rc = rc ? rc : launch_base_pd(h);
   if (rc) return rc;
-  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
-                     dim3(grid_for(n, 256)), dim3(256), lds_bytes(h), h->stream, h->s0.p,
-                     (long long)n, h->scene(), h->geo(), h->i0.p, 1);
+  // robot vs obstacles only (pairwise_collision(robot, b) for b in obstacles): the arm's
+  // self pairs of tcmp_set_self_collision are not part of the body-level check
+  Scene sc = h->scene();
+  sc.self_coll = 0;
+  const bool mk = h->n_mesh > 0;
+  hipLaunchKernelGGL(mk ? k_check_configs<true> : k_check_configs<false>,
+                     dim3(grid_for(n, 256)), dim3(256),
+                     mk ? stage_lds_bytes_lean(h->n_obs) : stage_lds_bytes(h->n_obs), h->stream,
+                     h->s0.p, (long long)n, sc, h->geo(), h->i0.p, 1);
   HIPCHK(hipGetLastError());
   const int nb = h->n_box + h->n_mesh;
   if (nb) {
@@ -3109,6 +3132,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   r->ms_nn_scan = h->ms[F_NNSCAN];
   r->snap_sum = s.snap_sum;
   r->nn_full_pairs = s.nn_full_pairs;
+  r->n_rewires = s.rewires;
   return 0;
 }
 

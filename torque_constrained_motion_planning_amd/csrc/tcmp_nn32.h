@@ -1,5 +1,6 @@
-// tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with a
-// 16-bit first pass.  Included by tcmp_engine.hip after tcmp_nn.h.
+// tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with an fp32
+// first pass (the default build; TCMP_NN_Q16 swaps in 16-bit rows, below).  Included by
+// tcmp_engine.hip after tcmp_nn.h.
 //
 // Every (candidate, node) pair is first evaluated in fp32 on the f32 rows srow (half the bytes
 // of the fp64 rows, twice the VALU rate).  A node is re-evaluated exactly in fp64 (the same

@@ -232,11 +232,13 @@ class _Tree:
 
 
 def _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam_fn, radius,
-              max_time=INF, max_iterations=INF, goal_probability=.2, informed=False, kinds=None):
+              max_time=INF, max_iterations=INF, goal_probability=.2, informed=False, kinds=None,
+              stats=None):
     """rrt_star.py:151-211 with the tree on the host, for foreign distance / extend callbacks.
     Callback call order is the reference's, except that the package's
     own collision and torque tests are evaluated for a whole extend sequence at once (they
-    are pure functions, so that is unobservable)."""
+    are pure functions, so that is unobservable).  stats (a dict, optional) receives the final
+    tree ("tree": _Tree) and the rewire count ("n_rewires")."""
     k = kinds if kinds is not None else _kinds(distance, sample, extend, collision, torque_fn,
                                                dynam_fn)
     eng = collision.engine if k["collision"] else None
@@ -283,6 +285,7 @@ def _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam
 
     tree = _Tree(start)
     goal_n = None
+    n_rewires = 0
     t0 = time()
     it = 0
     while (t0 - time()) < max_time and it < max_iterations:  # (sic) rrt_star.py:159
@@ -310,6 +313,9 @@ def _rrt_host(start, goal, distance, sample, extend, collision, torque_fn, dynam
                 end, pts = safe_prefix(tree.configs[n], last)
                 if end is not None and distance(last, end) < 1e-6:
                     tree.reparent(new, n, d, pts)
+                    n_rewires += 1
+    if stats is not None:
+        stats.update(tree=tree, n_rewires=n_rewires)
     if goal_n is None:
         print("failed to find goal")
         return None, None, None, None
