@@ -499,6 +499,17 @@ def main():
         # proof of the collective world the run used: RCCL's own rank count, and rank 0's check
         # that every gather delivered every query id with the all-gathered row counts
         line["rccl_ranks"] = comm.rccl_ranks()
+        # every rank's drawn samples (replica / sharded mode: each rank's own trees)
+        per_rank = comm.allgather_i64([int(sum(x["n_samples"] for x in results))])
+        line["samples_per_rank"] = [int(v) for v in per_rank[:, 0]]
+        if shared:
+            # proof that the ranks grew ONE tree: the device digest of the last step's tree
+            # (tcmp_plan_digest), all-gathered; equal digests and node counts on every rank
+            d, nn = eng.plan_digest()
+            g = comm.allgather_i64([d - (1 << 64) if d >= (1 << 63) else d, nn])
+            line["tree_consistent"] = bool((g == g[0]).all())
+            line["tree_digest"] = "%016x" % d
+            line["tree_nodes"] = int(nn)
         if not shared:
             line["gather_ok"] = bool(GATHER["ok"])
             line["gathered"] = {"queries": GATHER["queries"], "rows": GATHER["rows"],

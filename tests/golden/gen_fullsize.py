@@ -3,7 +3,9 @@ build container, never on the GPU box).
 
 The bench's own headline query -- bench.py make_query(1234) on the C3 workload (16 boxes,
 5 kg, rne, 1e6 samples, B = 262,144, seed 1234 = step_seed(0) of rank 0) -- and a C5 query
-(bench.py make_query(1234, n_mesh=256), 2e5 samples, B = 262,144) are planned by the
+(bench.py make_query(1234, n_mesh=256), 131,072 samples in eight rounds of B = 16,384, Philox
+seed 1243 -- the goal is reached in the last rounds, so waypoints, min-jerk and the final
+validation are covered; tools/c5_fixture_search.py found the seed on the GPU) are planned by the
 oracle's batched restatement of rrt_star.py:151-211 (oracle/tcmp_oracle.c orc_rrt_run,
 OpenMP over the lanes of a round; insertion stays in lane order).  The scene is generated
 by bench.py's make_query itself, with the oracle standing in for the engine's collision /
@@ -107,4 +109,4 @@ if __name__ == "__main__":
     if "c3" in which:
         make("c3", 16, 0, 1_000_000, 262144, 1234)
     if "c5" in which:
-        make("c5", 0, 256, 200_000, 262144, 1234)
+        make("c5", 0, 256, 131_072, 16384, 1243)

@@ -140,3 +140,29 @@ def test_group_rejects_bad_shapes():
         _lib.plan_run_group(es, 4000, 2048)   # 1024 lanes per engine > max_batch 512
     with pytest.raises(_lib.TcmpError):
         _lib.plan_run_group(es, 4000, 1)      # fewer lanes than engines
+
+
+def test_tree_digest_proves_one_tree():
+    """tcmp_plan_digest (what bench.py --shared-tree all-gathers as tree_consistent): the
+    engines of a group round report the lone engine's digest; the host restatement
+    (shard.tree_digest) over the fetched tree gives the same value; a different tree
+    (another seed) gives another."""
+    from torque_constrained_motion_planning_amd import _lib, shard
+    obs, goal = _query(71, 16, 2, 5.0)
+    n, batch = 20_000, 4096
+    one = _lib.Engine(0)
+    _begin(one, obs, goal, 2, 5.0, n, batch, 5)
+    one.plan_run(n, batch)
+    es = [_lib.Engine(0) for _ in range(3)]
+    for e in es:
+        _begin(e, obs, goal, 2, 5.0, n, -(-batch // 3), 5)
+    _lib.plan_run_group(es, n, batch)
+    d1, n1 = one.plan_digest()
+    cfg, cost, par, m = _tree(one, n)
+    assert n1 == m > 1000
+    assert shard.tree_digest(cfg, cost, par) == d1
+    assert [e.plan_digest() for e in es] == [(d1, n1)] * 3
+    other = _lib.Engine(0)
+    _begin(other, obs, goal, 2, 5.0, n, batch, 6)
+    other.plan_run(n, batch)
+    assert other.plan_digest()[0] != d1

@@ -7,6 +7,10 @@
 #   trace[=W]        rocprofv3 --kernel-trace --stats of the same bench command
 #   pmc[=W]          PMC passes FETCH_SIZE / WRITE_SIZE (one run each) over one bench step
 #   sq[=W]           PMC pass of SQ wave / busy counters over one bench step
+#   prof             profiling-build (make prof) clock breakdowns: tools/nn_profile.py and
+#                    tools/edge_profile.py on C3
+#   ab=LIBS          same-box A/B of libtcmp builds (space-separated .so paths): C3 bench lines,
+#                    two passes (tools/ab_lib.sh; bench arguments via env:AB_ARGS=...)
 #   env:VAR=V        export VAR=V for the following stages (A/B knobs, TCMP_LIB_PATH=...)
 # Outputs under gpurun_out/TAG/.
 set -e -o pipefail
@@ -51,6 +55,12 @@ for st in "$@"; do
         --kernel-trace -d $O/sq_$w -o run --output-format csv \
         -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
         --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
+    prof)
+      P=torque_constrained_motion_planning_amd/libtcmp_prof.so
+      TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err
+      TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/edge_profile.py 2 > $O/edge_profile.json 2> $O/edge_profile.err ;;
+    ab)
+      bash tools/ab_lib.sh $TAG/ab "$arg" ${AB_ARGS:-} ;;
     env:*)
       export "${st#env:}" ;;
     *) echo "unknown stage $st" >&2; exit 2 ;;

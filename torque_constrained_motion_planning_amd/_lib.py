@@ -30,7 +30,7 @@ EXPORTS = [
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_retrace",
     "tcmp_plan_run_shared", "tcmp_plan_run_group",
-    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
+    "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_digest", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
     "tcmp_dist_barrier", "tcmp_dist_allreduce", "tcmp_dist_allgather_i64", "tcmp_gather_paths",
@@ -132,6 +132,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_plan_retrace.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
         L.tcmp_plan_tree.argtypes = [vp, ctypes.c_int64, _dp, _dp, _i32p, _i64p]
+        if hasattr(L, "tcmp_plan_digest"):  # absent from A/B builds of older sources
+            L.tcmp_plan_digest.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), _i64p]
         L.tcmp_plan_debug_round.argtypes = [vp, ctypes.c_int64, _dp, _i32p, _dp, _i64p, _i32p]
         L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
         L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
@@ -425,6 +427,14 @@ class Engine:
         qdd = np.zeros((K, 7)); psg = np.zeros(K); tau = np.zeros((K, 7))
         self._check(self.L.tcmp_plan_fetch(self.h, _d(wp), _d(q), _d(qd), _d(qdd), _d(psg), _d(tau)))
         return dict(waypoints=wp, q=q, qd=qd, qdd=qdd, psg=psg, tau=tau)
+
+    def plan_digest(self):
+        """(digest, n_nodes) of the open plan's tree, computed on the device (tcmp_plan_digest;
+        shard.tree_digest restates it on the host)."""
+        d = ctypes.c_uint64(0)
+        n = ctypes.c_int64(0)
+        self._check(self.L.tcmp_plan_digest(self.h, ctypes.byref(d), ctypes.byref(n)))
+        return int(d.value), int(n.value)
 
     def plan_tree(self, cap):
         cfg = np.zeros((cap, 7)); cost = np.zeros(cap); par = np.zeros(cap, dtype=np.int32)

@@ -695,7 +695,8 @@ __device__ unsigned long long g_exact_stats[24];  // [4..7]: mesh pairs (exact_p
                                                   // [16..20]: exact_pair mesh-stage clocks
 #endif
 __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
-                                              const double* __restrict__ ob, const Geo g) {
+                                              const double* __restrict__ ob, const Geo g,
+                                              const float4* __restrict__ balls = nullptr) {
   const int lane = lane_id();
   const double* R = pose.R;
   const double* p = pose.p;
@@ -740,6 +741,69 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
     if (lane == 0) atomicAdd(&g_exact_stats[0], 1ull);
 #endif
     return pd;
+  }
+  if (balls) {
+    // Inscribed-ball certificates (box obstacles), wave-cooperative: the link's TCMP_NSPH
+    // balls (inside its hull), one per lane, in the box frame x = A^T (s - cl).  A ball whose
+    // centre is inside the box penetrates it by exactly r + min_j (h_j - |x_j|), a lower bound
+    // of the pair's depth (monotone under inclusion): "collision" at kPen + guard and above.
+    // Otherwise the best ball's direction to its closest box point (inside: its nearest
+    // face's inward normal) is a trial axis a, and the hull's support along it (its vertices)
+    // against the box's exact support overlapping by less than kPen - guard proves "free".
+    // fp32, errors far inside the guard, so the decision is the exact test's.
+    float x0 = 0.f, x1 = 0.f, x2 = 0.f, v = -INFINITY, sl = -INFINITY;
+    if (lane < TCMP_NSPH) {
+      const float4 b = balls[lane];
+      const float s0 = b.x - cl[0], s1 = b.y - cl[1], s2 = b.z - cl[2];
+      x0 = A[0] * s0 + A[3] * s1 + A[6] * s2;
+      x1 = A[1] * s0 + A[4] * s1 + A[7] * s2;
+      x2 = A[2] * s0 + A[5] * s1 + A[8] * s2;
+      const float e0 = fabsf(x0) - h[0], e1 = fabsf(x1) - h[1], e2 = fabsf(x2) - h[2];
+      sl = -fmaxf(e0, fmaxf(e1, e2));
+      const float o0 = fmaxf(e0, 0.f), o1 = fmaxf(e1, 0.f), o2 = fmaxf(e2, 0.f);
+      v = sl >= 0.f ? b.w + sl : b.w - __builtin_sqrtf(o0 * o0 + o1 * o1 + o2 * o2);
+    }
+    const float vb = wave_maxf(v);
+    const int L = __builtin_ctzll(__ballot(v == vb));
+    const float bs = __shfl(sl, L);
+    if (bs >= 0.f && vb >= P + kExactGuard) {
+#ifdef TCMP_PROF_EXACT
+      if (lane == 0) atomicAdd(&g_exact_stats[21], 1ull);
+#endif
+      return vb;
+    }
+    x0 = __shfl(x0, L); x1 = __shfl(x1, L); x2 = __shfl(x2, L);
+    float a0, a1, a2;
+    if (bs < 0.f) {
+      a0 = fminf(fmaxf(x0, -h[0]), h[0]) - x0;
+      a1 = fminf(fmaxf(x1, -h[1]), h[1]) - x1;
+      a2 = fminf(fmaxf(x2, -h[2]), h[2]) - x2;
+    } else {
+      const float s0 = h[0] - fabsf(x0), s1 = h[1] - fabsf(x1), s2 = h[2] - fabsf(x2);
+      a0 = (s0 <= s1 && s0 <= s2) ? (x0 < 0.f ? 1.f : -1.f) : 0.f;
+      a1 = (a0 == 0.f && s1 <= s2) ? (x1 < 0.f ? 1.f : -1.f) : 0.f;
+      a2 = (a0 == 0.f && a1 == 0.f) ? (x2 < 0.f ? 1.f : -1.f) : 0.f;
+    }
+    const float l2 = a0 * a0 + a1 * a1 + a2 * a2;
+    if (l2 > 1e-12f) {
+      const float il = rsqrtf(l2);
+      a0 *= il; a1 *= il; a2 *= il;
+      // the axis in the link frame, l = A a; overlap = max_v v.l - cl.l + sum_j h_j |a_j|
+      const float lx = A[0] * a0 + A[1] * a1 + A[2] * a2;
+      const float ly = A[3] * a0 + A[4] * a1 + A[5] * a2;
+      const float lz = A[6] * a0 + A[7] * a1 + A[8] * a2;
+      float hl = -INFINITY;
+      for (int w = v0 + lane; w < v1; w += 64)
+        hl = fmaxf(hl, g.verts32[3 * w] * lx + g.verts32[3 * w + 1] * ly + g.verts32[3 * w + 2] * lz);
+      const float ov = wave_maxf(hl) - (cl[0] * lx + cl[1] * ly + cl[2] * lz) +
+                       h[0] * fabsf(a0) + h[1] * fabsf(a1) + h[2] * fabsf(a2);
+      if (ov < P - kExactGuard) {
+#ifdef TCMP_PROF_EXACT
+        if (lane == 0) atomicAdd(&g_exact_stats[22], 1ull);
+#endif
+        return ov;
+      }
+    }
   }
   float loc = INFINITY;
   for (int f = f0 + lane; f < f1; f += 64) {
@@ -970,7 +1034,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     return (const double*)slot;
   };
   if (!MESH || mi < 0) {
-    const float pd32 = exact_pd_wave32(link, pose(), ob, g);
+    const float pd32 = exact_pd_wave32(link, pose(), ob, g,
+                                       sc.box_cert ? sc.csph + TCMP_NSPH * link : nullptr);
     if (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) return (double)pd32;
     return exact_pd_wave(link, pose_to_lds(), ob, g.verts, g.planes, g.edges);
   }
@@ -1297,6 +1362,18 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
     aabb[i] = bx[12] * fabs(U[3 * i + 0]) + bx[13] * fabs(U[3 * i + 1]) + bx[14] * fabs(U[3 * i + 2]);
 }
 
+#ifndef TCMP_SC_JUNROLL
+#define TCMP_SC_JUNROLL 4   // sphere_cert's ball-pair loops: mesh balls (outer) ...
+#endif
+#ifndef TCMP_SC_IUNROLL
+#define TCMP_SC_IUNROLL 16  // ... and link balls (inner)
+#endif
+#ifndef TCMP_SC_UNROLL
+#define TCMP_SC_UNROLL 8  // stream unroll of sphere_cert's LOD / vertex loops
+#endif
+#ifndef TCMP_SPHERE_CERT
+#define TCMP_SPHERE_CERT 1  // 0: no lane-parallel sphere certificates in phase B (A/B builds)
+#endif
 #ifndef TCMP_CERT_INLINE
 #define TCMP_CERT_INLINE __forceinline__
 #endif
@@ -1311,26 +1388,22 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 // far inside the 1e-4 guard, so the decision is the exact test's.  Returns 0 free,
 // 1 collision, 2 undecided.  Mesh m: rows TCMP_NSPH * (10 + m) of sph, world frame (link
 // meshes of self pairs: their own link frame, as the pose is then).
-__device__ TCMP_CERT_INLINE int sphere_cert(int link, const double Rd[9], const double pd[3], int mi,
+__device__ TCMP_CERT_INLINE int sphere_cert(int link, const float R[9], const float p[3], int mi,
                                             const Scene sc, const Geo g) {
-  float R[9], p[3];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) R[k] = (float)Rd[k];
-#pragma unroll
-  for (int k = 0; k < 3; ++k) p[k] = (float)pd[k];
   const float4* LS = sc.csph + TCMP_NSPH * link;               // LDS (mesh kernels)
   const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);  // global
   // every mesh ball into the link frame once (u = R^T (t - p)), against the link's balls;
   // best: the largest overlap r_i + r_j - |u_j - s_i|, its link-frame direction s_i -> u_j
   float best = -INFINITY, ax = 1.f, ay = 0.f, az = 0.f;
   int bi = 0, bj = 0;
-#pragma unroll 4
+#pragma unroll TCMP_SC_JUNROLL
   for (int j = 0; j < TCMP_NSPH; ++j) {
     const float4 t = MS[j];
     const float dx = t.x - p[0], dy = t.y - p[1], dz = t.z - p[2];
     const float ux = R[0] * dx + R[3] * dy + R[6] * dz;
     const float uy = R[1] * dx + R[4] * dy + R[7] * dz;
     const float uz = R[2] * dx + R[5] * dy + R[8] * dz;
+#pragma unroll TCMP_SC_IUNROLL
     for (int i = 0; i < TCMP_NSPH; ++i) {
       const float4 s = LS[i];
       const float ex = ux - s.x, ey = uy - s.y, ez = uz - s.z;
@@ -1353,7 +1426,7 @@ __device__ TCMP_CERT_INLINE int sphere_cert(int link, const double Rd[9], const 
       const float ly = R[1] * dx + R[4] * dy + R[7] * dz;
       const float lz = R[2] * dx + R[5] * dy + R[8] * dz;
       const int f1 = tcmp_lod_in_plane_off[link + 1];
-#pragma unroll 8
+#pragma unroll TCMP_SC_UNROLL
       for (int f = tcmp_lod_in_plane_off[link]; f < f1; ++f) {
         const float4 n = sc.lodpl[0][f];
         sl = fminf(sl, n.w - (n.x * lx + n.y * ly + n.z * lz));
@@ -1366,7 +1439,7 @@ __device__ TCMP_CERT_INLINE int sphere_cert(int link, const double Rd[9], const 
       const float cy = R[3] * s.x + R[4] * s.y + R[5] * s.z + p[1];
       const float cz = R[6] * s.x + R[7] * s.y + R[8] * s.z + p[2];
       const int f1 = rg[9];
-#pragma unroll 8
+#pragma unroll TCMP_SC_UNROLL
       for (int f = rg[8]; f < f1; ++f) {
         const float4 n = sc.lp32[0][f];
         sm = fminf(sm, n.w - (n.x * cx + n.y * cy + n.z * cz));
@@ -1387,12 +1460,12 @@ __device__ TCMP_CERT_INLINE int sphere_cert(int link, const double Rd[9], const 
     // overlap along a: the link's support (its vertices, LDS) minus the mesh's minimum
     float hl = -INFINITY;
     const int v1 = tcmp_geo_vert_off[link + 1];
-#pragma unroll 4
+#pragma unroll TCMP_SC_UNROLL
     for (int v = tcmp_geo_vert_off[link]; v < v1; ++v)
       hl = fmaxf(hl, sc.cv32[3 * v] * bx + sc.cv32[3 * v + 1] * by + sc.cv32[3 * v + 2] * bz);
     float hm = INFINITY;
     const int w1 = rg[1];
-#pragma unroll 8
+#pragma unroll TCMP_SC_UNROLL
     for (int w = rg[0]; w < w1; ++w) {
       const float4 x = sc.mv32[w];
       hm = fminf(hm, x.x * ax + x.y * ay + x.z * az);
@@ -1621,11 +1694,24 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #endif
         }
       }
-      if (MESH) {
-        // lane-parallel sphere certificates before the wave-serial exact chain
-        const bool sp = cls == 2 && mi >= 0 && sc.mrange[kMrange * mi + 19] != 0;
+      if (MESH && __ballot(cls == 2)) {
+        // the undecided pairs' poses go to the stash: R / p (fp64) die here instead of living
+        // across the sphere certificates and every hull-vs-hull test of the wave
+        double* ps = stash + 14 * 64;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) ps[k * 64 + lane] = R[k];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ps[(9 + k) * 64 + lane] = p[k];
+        __asm__ volatile("" ::: "memory");
+        // lane-parallel sphere certificates before the wave-serial exact chain (fp32 pose)
+        const bool sp = TCMP_SPHERE_CERT && cls == 2 && mi >= 0 && sc.mrange[kMrange * mi + 19] != 0;
         if (__ballot(sp) && sp) {
-          cls = sphere_cert(lk, R, p, mi, sc, g);
+          float Rf[9], pf[3];
+#pragma unroll
+          for (int k = 0; k < 9; ++k) Rf[k] = (float)ps[k * 64 + lane];
+#pragma unroll
+          for (int k = 0; k < 3; ++k) pf[k] = (float)ps[(9 + k) * 64 + lane];
+          cls = sphere_cert(lk, Rf, pf, mi, sc, g);
 #ifdef TCMP_PROF_EXACT
           if (cls != 2) atomicAdd(&g_exact_stats[cls ? 14 : 15], 1ull);
 #endif
@@ -1633,16 +1719,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       }
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
-      if (MESH && pend) {
-        // the pending pairs' poses go to the stash: R / p die here instead of living across
-        // every hull-vs-hull test of the wave
-        double* ps = stash + 14 * 64;
-#pragma unroll
-        for (int k = 0; k < 9; ++k) ps[k * 64 + lane] = R[k];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) ps[(9 + k) * 64 + lane] = p[k];
-        __asm__ volatile("" ::: "memory");
-      }
       while (pend) {
         const int L = __builtin_ctzll(pend);
         pend &= pend - 1;
@@ -1664,7 +1740,13 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
 #endif
+#ifdef TCMP_DIAG_NOEXACT
+        // diagnostic builds only (wrong results): undecided pairs collide, no exact test
+        const double pd = kPen;
+        (void)ob;
+#else
         const double pd = exact_pair<MESH>(lL, PL, MESH ? stash + 14 * 64 + L : nullptr, ob, sc, g);
+#endif
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif
@@ -1776,8 +1858,18 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         count += (int)__popcll(bm);
       }
     }
+#ifdef TCMP_DIAG_NOPHASEB
+    // diagnostic builds only (wrong results): every queued pair collides, no phase B
+    if (count) {
+      for (int b = 0; b < count; b += 64)
+        if (b + lane < count) atomicOr(cmask, 1ull << (queue[b + lane] & 63u));
+      __builtin_amdgcn_wave_barrier();
+      count = 0;
+    }
+#else
     // one flush call site (a full queue always holds pairs): phase B is inlined once
     if (count) flush();
+#endif
     if (!full) break;
   }
   __builtin_amdgcn_wave_barrier();

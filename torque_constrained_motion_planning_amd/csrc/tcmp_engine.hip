@@ -680,6 +680,33 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
 }
 
 // ------------------------------------------------------------------------------------------
+// tree digest (tcmp_plan_digest): sum over nodes i of mix(i, cfg bits, cost bits, parent) mod
+// 2^64 -- order-independent, so one reduction; two trees have the same digest iff (up to a
+// 2^-64 collision) every node's record is the same.  mix = splitmix64 chained over the words.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__global__ __launch_bounds__(256) void k_tree_digest(const DevState* st, const double* cfg,
+                                                     const int* parent, unsigned long long* out) {
+  const long long T = st->n_nodes;
+  unsigned long long acc = 0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < T; i += (long long)gridDim.x * 256) {
+    unsigned long long x = splitmix64((unsigned long long)i);
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      x = splitmix64(x ^ (unsigned long long)__double_as_longlong(cfg[8 * i + k]));
+    x = splitmix64(x ^ (unsigned long long)(unsigned)parent[i]);
+    acc += x;
+  }
+  acc = wave_sum_u64(acc);
+  if (lane_id() == 0 && acc) atomicAdd(out, acc);
+}
+
+// ------------------------------------------------------------------------------------------
 // retrace (rrt_star.py:42-45, 202): [start] + for each edge root->goal the first n_safe-1
 // regenerated extend points + the node's configuration.  One block.
 // ------------------------------------------------------------------------------------------
@@ -3156,6 +3183,26 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
     if (tau) HIPCHK(hipMemcpyAsync(tau, h->ttau.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_plan_digest(tcmp_handle* h, uint64_t* digest, int64_t* n_nodes) {
+  if (int rc = set_dev(h)) return rc;
+  if (!digest || !n_nodes) return fail(-1, "null argument");
+  if (!h->plan_open) return fail(-1, "no open plan");
+  if (int rc = h->u0.ensure(1)) return rc;
+  HIPCHK(hipMemsetAsync(h->u0.p, 0, sizeof(unsigned long long), h->stream));
+  long long cap = h->P.max_nodes;
+  hipLaunchKernelGGL(k_tree_digest, dim3(grid_for(std::min<long long>(cap, 1 << 20), 256)),
+                     dim3(256), 0, h->stream, h->st, h->cfg.p, h->parent.p, h->u0.p);
+  HIPCHK(hipGetLastError());
+  long long nn = 0;
+  unsigned long long d = 0;
+  HIPCHK(hipMemcpyAsync(&d, h->u0.p, sizeof(d), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipMemcpyAsync(&nn, &h->st->n_nodes, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
+  HIPCHK(hipStreamSynchronize(h->stream));
+  *digest = d;
+  *n_nodes = nn;
   return 0;
 }
 

@@ -85,3 +85,30 @@ def gather_ok(got, expect_ids, sizes):
         return False
     return sum(len(v) for v in got.values()) == int(sizes[:, 1].sum()) and \
         len(got) == int(sizes[:, 0].sum())
+
+
+_M64 = (1 << 64) - 1
+
+
+def _splitmix64(x):
+    """splitmix64 on a uint64 array (wrapping arithmetic)."""
+    with np.errstate(over="ignore"):
+        x = x + np.uint64(0x9E3779B97F4A7C15)
+        x = (x ^ (x >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        x = (x ^ (x >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return x ^ (x >> np.uint64(31))
+
+
+def tree_digest(cfg, cost, parent):
+    """Host restatement of tcmp_plan_digest over a tree (cfg n x 7, cost n, parent n): the
+    sum over nodes i of splitmix64 chained over (i, cfg[i] bits, cost[i] bits, parent[i]),
+    mod 2^64.  Ranks of a shared-tree run compare it to prove they hold one tree."""
+    cfg = np.ascontiguousarray(cfg, dtype=np.float64).reshape(-1, 7)
+    n = len(cfg)
+    words = np.concatenate([cfg, np.asarray(cost, dtype=np.float64).reshape(n, 1)], 1).view(np.uint64)
+    x = _splitmix64(np.arange(n, dtype=np.uint64))
+    for k in range(8):
+        x = _splitmix64(x ^ words[:, k])
+    x = _splitmix64(x ^ np.asarray(parent, dtype=np.int32).astype(np.uint32).astype(np.uint64))
+    return int(x.astype(object).sum()) & _M64
+
