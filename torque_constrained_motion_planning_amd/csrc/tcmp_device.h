@@ -1137,10 +1137,11 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 // (4) otherwise the exact wave-cooperative hull test.  (1)-(3) are conservative bounds of
 // (4) (inner box subset hull subset outer OBB), so the answer is exactly (4)'s.
 // ------------------------------------------------------------------------------------------
+// wave totals (wave-uniform: popcounts of ballots, so they stay in SGPRs)
 struct StepStats {
   unsigned pairs_tested;  // tier-1 tests
   unsigned pairs_sat;     // tier-2/3 evaluations
-  unsigned pairs_exact;   // tier-4 evaluations (wave-level count, lane 0)
+  unsigned pairs_exact;   // tier-4 evaluations
 #ifdef TCMP_PROF
   unsigned long long cyc_exact = 0;  // shader clocks spent in tier 4 (profiling builds)
   unsigned long long cyc_t123 = 0;   // ... in tiers 1-3 (maybe branch, excluding tier 4)
@@ -1208,7 +1209,7 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
                                              const double wc[3], const double U[9],
                                              const double aabb[3],
                                              const double* __restrict__ ob,
-                                             const double* __restrict__ hin, StepStats& st) {
+                                             const double* __restrict__ hin, bool& sat) {
   const double* bx = tcmp_geo_boxes + 18 * link;
   const double h0 = ob[12], h1 = ob[13], h2 = ob[14];
   const bool aligned = ob[15] > 0.0;
@@ -1230,7 +1231,7 @@ __device__ __forceinline__ int classify_pair(int link, const double R[9], const 
       if ((ob[12 + k] + r) - fabs(dk) < kPen) return 0;
     }
   }
-  st.pairs_sat++;
+  sat = true;
   // tiers 2/3: 15-axis SAT in the link-box frame (M = U^T B, t = U^T (c - w))
   double M[9], aM[9], t[3];
 #pragma unroll
@@ -1678,12 +1679,13 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         for (int k = 0; k < 3; ++k) p[k] = pr[k];
       }
       int cls = 0, mi = -1;
+      bool sat = false;
       if (has) {
         double wc[3], U[9], aabb[3];
         link_obb(lk, R, p, wc, U, aabb);
         const double* ob = sc.obs + 16 * orow;
         mi = MESH ? obs_mesh(ob) : -1;
-        cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, st);
+        cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, sat);
         // boxes: the lane-parallel ball / trial-axis certificate before the wave-serial exact
         // test -- measured slower on C3 (its registers cost more than the exact tests it
         // saves), so a build knob, off
@@ -1717,6 +1719,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #endif
         }
       }
+      st.pairs_sat += (unsigned)__popcll(__ballot(sat));
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
       while (pend) {
@@ -1750,10 +1753,8 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif
-        if (lane == 0) {
-          st.pairs_exact++;
-          if (pd >= kPen) atomicOr(cmask, 1ull << sL);
-        }
+        st.pairs_exact++;
+        if (lane == 0 && pd >= kPen) atomicOr(cmask, 1ull << sL);
       }
     }
     __builtin_amdgcn_wave_barrier();
@@ -1763,7 +1764,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #endif
   };
   // ---- phase A ------------------------------------------------------------------------
-  if (live) st.pairs_tested += 10u * (unsigned)sc.n_obs;
+  st.pairs_tested += 10u * (unsigned)sc.n_obs * (unsigned)__popcll(__ballot(live));
   // A queue that fills up is flushed after the loop and phase A resumes at (o_res, l_res);
   // the link AABBs are rebuilt on resume, so nothing of phase A is live across a flush.
   int o_res = 0, l_res = 0;

@@ -380,7 +380,7 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 #pragma unroll
   for (int k = 0; k < 7; ++k) q[k] = 0.5 * (kLo[k] + kHi[k]);
   StepStats ss = {};
-  unsigned steps = 0;  // this lane's extend steps (32-bit: one register)
+  unsigned steps = 0;  // extend steps: the wave's (SPLIT == 1, uniform) or this lane's
 #ifdef TCMP_PROF
   unsigned long long c_total = 0, c_fetch = 0, c_coll = 0, c_torque = 0, c_tail = 0, c_sincos = 0;
   const unsigned long long c_start = clock64();
@@ -461,8 +461,8 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 #endif
     const bool ok = active && !coll && tok;
     if (SPLIT == 1) {
+      steps += (unsigned)__popcll(__ballot(active));  // wave total
       if (active) {
-        ++steps;
         if (ok) {
           double q2[7];
           load7(J.to + 8 * (size_t)e, q2);
@@ -507,8 +507,10 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
     c_tail += clock64() - c0;
 #endif
   }
-  const unsigned long long a = wave_sum_u64((unsigned long long)steps), b = wave_sum_u64(ss.pairs_tested),
-                           c = wave_sum_u64(ss.pairs_sat), d = wave_sum_u64(ss.pairs_exact);
+  // steps: a wave total for SPLIT == 1, per group leader otherwise; ss: wave totals
+  const unsigned long long a = SPLIT == 1 ? (unsigned long long)steps
+                                          : wave_sum_u64((unsigned long long)steps),
+                           b = ss.pairs_tested, c = ss.pairs_sat, d = ss.pairs_exact;
   if (lane == 0) {
     atomicAdd(&st->edge_steps, a);
     atomicAdd(&st->pairs_tested, b);
@@ -849,7 +851,7 @@ __device__ __forceinline__ void sincos7(const double q[7], double cq[7], double 
 // dynam_fn + final validation for the planner's path, one row per thread; Conf.torques follow
 // in k_traj_tau (one RNE per kernel keeps both at two waves per SIMD)
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? 1 : 2))) void k_traj(const PlanParams* __restrict__ Pd, DevState* st, const double* wp,
                        double* oq, double* oqd, double* oqdd, double* opsg, long long kcap) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (st->goal_node < 0) return;
@@ -872,7 +874,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k
 }
 
 // Conf.torques of the path's rows: rne without payload (utils.py:3376)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_traj_tau(const DevState* st, const double* q, const double* qd,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void k_traj_tau(const DevState* st, const double* q, const double* qd,
                            const double* qdd, double* otau, long long kcap) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (st->goal_node < 0) return;
@@ -929,7 +931,7 @@ __global__ __launch_bounds__(256) void k_check_configs(const double* q, long lon
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_torque(const double* q, const double* qd, const double* qdd, long long n,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? 1 : 2))) void k_torque(const double* q, const double* qd, const double* qdd, long long n,
                          double mass, int* ok) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -968,7 +970,7 @@ __global__ void k_minjerk(const double* wp, long long nwp, long long ni, double*
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_validate(const double* q, const double* qd, const double* qdd, long long n,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(MODE == 3 ? 1 : 2))) void k_validate(const double* q, const double* qd, const double* qdd, long long n,
                            double mass, unsigned long long* first_fail) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
