@@ -268,6 +268,9 @@ def main():
     ap.add_argument("--samples", type=int, default=None, help="samples per query")
     ap.add_argument("--batch", type=int, default=None)
     ap.add_argument("--obstacles", type=int, default=None, help="boxes per scene")
+    ap.add_argument("--queries", type=int, default=None,
+                    help="queries per step over all ranks (c4: 64; --queries 8 on one GPU is "
+                         "one GPU's share of c4 at N = 8)")
     ap.add_argument("--cpu-samples", type=int, default=40000)
     ap.add_argument("--cpu-workers", type=int, default=usable_cores(),
                     help="worker processes of the multi-core CPU baseline (default: every "
@@ -301,6 +304,8 @@ def main():
         W["batch"] = args.batch
     if args.obstacles is not None:
         W["boxes"] = args.obstacles
+    if args.queries is not None and W["queries"] > 1:
+        W["queries"] = args.queries
     shared = args.shared_tree and W["queries"] == 1
     if shared:
         W["scaling"] = "strong"
@@ -313,6 +318,11 @@ def main():
     n_obs_total = W["boxes"] + W["meshes"]
 
     eng = _lib.Engine(gpu)
+    # the spec peaks re-measured on this device, reported beside the spec figures
+    try:
+        measured = eng.microbench()
+    except _lib.TcmpError as e:  # older library builds (A/B runs) lack the entry point
+        measured = {"error": str(e)}
     # query ids of this rank: c4 shards 64 queries round-robin (scene and goal fixed per query
     # id); the single-query workloads run the same scene (query id 0) on every rank with
     # rank-dependent sample seeds -- independent trees of identical expected work, so the
@@ -453,6 +463,10 @@ def main():
             # the PMC flop per launch over this run's event-timed average launch
             mv["tflops_live"] = mv["flop_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
             mv["frac_live"] = mv["tflops_live"] / peak
+    for roof, key in ((roof_nn, "fp32_tflops"), (roof_ed, "fp64_tflops")):
+        if measured.get(key):
+            roof["peak_measured"] = measured[key]
+            roof["frac_measured"] = roof["achieved"] / measured[key]
     dominant, other = (roof_nn, roof_ed) if nn_ms >= ed_ms else (roof_ed, roof_nn)
     # north-star HBM figure: compulsory bytes per query = 68 T_r per round (tree read
     # once) + 72 B_r per round (candidates written) + trajectory rows, over the step time
@@ -460,6 +474,7 @@ def main():
     hbm_bytes = 68 * snap + 72 * sum(x["n_samples"] for x in results) + \
         22 * 8 * sum(x["n_traj"] for x in results)
     hbm_gbs = hbm_bytes / (dt / 1.0) / 1e9 * world if dt > 0 else 0.0
+    hbm_peak_meas = measured.get("hbm_gbs")
 
     line = {
         "metric": "torque-feasible collision-checked RRT* samples/sec, Panda 7-DOF, 1/2/4/8 GPU",
@@ -485,8 +500,10 @@ def main():
         "roofline_other": other,
         "hbm_roofline": {"bytes_per_step": hbm_bytes / S, "achieved": hbm_gbs, "unit": "GB/s",
                          "peak": PEAK_HBM_GBS, "frac": hbm_gbs / PEAK_HBM_GBS,
+                         "peak_measured": hbm_peak_meas,
                          "definition": "SURVEY 8d compulsory bytes: 68 T_r + 72 B_r per round "
                                        "+ 176 B per trajectory row, whole job"},
+        "measured_peaks": measured,
         "kernel_ms_per_step": kernel_ms,
         # host wall time inside the C-ABI calls (rank 0; the GPU work of a step completes
         # inside plan_finish's first wait, so "finish" holds most of the step)

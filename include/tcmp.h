@@ -49,6 +49,12 @@ int tcmp_synchronize(tcmp_handle* h);
  * counts (36..43), n <= 44; zeros otherwise. */
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n);
 
+/* Peak microbenchmarks on the handle's device (the spec peaks are re-measured
+ * before use): out[0] fp64 vector FMA TFLOP/s, out[1] fp32 packed (v_pk_fma_f32) TFLOP/s,
+ * out[2] HBM GB/s of a 1 GiB float4 device copy (read + write bytes), out[3] 0.  Best of five
+ * launches each; allocates 2 GiB for the copy while it runs.  No reference counterpart. */
+int tcmp_microbench(tcmp_handle* h, double* out);
+
 /* Fixed obstacles (replaces Problem.fixed bodies + pybullet getClosestPoints,
  * utils.py:3165-3218 / 2833-2849).  n_obs oriented boxes, 15 doubles each:
  * centre(3), rotation R (9, row-major, columns = box axes, world frame), half extents(3). */

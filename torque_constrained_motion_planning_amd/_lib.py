@@ -31,7 +31,7 @@ EXPORTS = [
     "tcmp_plan_retrace",
     "tcmp_plan_run_shared", "tcmp_plan_run_group",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_digest", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
-    "tcmp_debug_counters",
+    "tcmp_debug_counters", "tcmp_microbench",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
     "tcmp_dist_barrier", "tcmp_dist_allreduce", "tcmp_dist_allgather_i64", "tcmp_gather_paths",
     "tcmp_gather_layout", "tcmp_dist_rccl_ranks",
@@ -138,6 +138,8 @@ def load_library(path=LIB_PATH):
         L.tcmp_ik.argtypes = [vp, _dp, _dp, ctypes.c_int64, _dp, _i32p]
         L.tcmp_fk.argtypes = [vp, _dp, ctypes.c_int64, _dp]
         L.tcmp_debug_counters.argtypes = [vp, ctypes.POINTER(ctypes.c_uint64), ctypes.c_int32]
+        if hasattr(L, "tcmp_microbench"):  # absent from A/B builds of older sources
+            L.tcmp_microbench.argtypes = [vp, _dp]
         i32 = ctypes.c_int32
         L.tcmp_rendezvous.argtypes = [i32, i32, ctypes.c_char_p, i32, vp, i32, i32]
         L.tcmp_dist_init.argtypes = [i32, i32, i32, ctypes.c_char_p, i32, ctypes.POINTER(vp)]
@@ -427,6 +429,14 @@ class Engine:
         qdd = np.zeros((K, 7)); psg = np.zeros(K); tau = np.zeros((K, 7))
         self._check(self.L.tcmp_plan_fetch(self.h, _d(wp), _d(q), _d(qd), _d(qdd), _d(psg), _d(tau)))
         return dict(waypoints=wp, q=q, qd=qd, qdd=qdd, psg=psg, tau=tau)
+
+    def microbench(self):
+        """Measured peaks of this device (tcmp_microbench): fp64 / packed-fp32 vector TFLOP/s
+        and HBM GB/s of a 1 GiB device copy."""
+        out = np.zeros(4)
+        self._check(self.L.tcmp_microbench(self.h, _d(out)))
+        return {"fp64_tflops": float(out[0]), "fp32_tflops": float(out[1]),
+                "hbm_gbs": float(out[2])}
 
     def plan_digest(self):
         """(digest, n_nodes) of the open plan's tree, computed on the device (tcmp_plan_digest;

@@ -698,6 +698,15 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g,
                                               const float4* __restrict__ balls = nullptr) {
   const int lane = lane_id();
+#ifdef TCMP_PROF_EXACT
+  // box pairs (balls != null): stage clocks in g_exact_stats[16..19] (box faces, balls,
+  // facets, edges) -- slots the mesh stages use in mesh scenes
+  unsigned long long tb = clock64();
+#define TCMP_BOX_CLK(i) if (balls) { const unsigned long long t1 = clock64(); \
+    if (lane == 0) atomicAdd(&g_exact_stats[16 + (i)], t1 - tb); tb = t1; }
+#else
+#define TCMP_BOX_CLK(i)
+#endif
   const double* R = pose.R;
   const double* p = pose.p;
   const double d[3] = {ob[0] - p[0], ob[1] - p[1], ob[2] - p[2]};
@@ -736,6 +745,7 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                fminf(fminf(mx1 - pc1 + h[1], pc1 + h[1] - mn1),
                      fminf(mx2 - pc2 + h[2], pc2 + h[2] - mn2)));
   }
+  TCMP_BOX_CLK(0);
   if (pd < P - kExactGuard) {
 #ifdef TCMP_PROF_EXACT
     if (lane == 0) atomicAdd(&g_exact_stats[0], 1ull);
@@ -805,6 +815,7 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
       }
     }
   }
+  TCMP_BOX_CLK(1);
   float loc = INFINITY;
   for (int f = f0 + lane; f < f1; f += 64) {
     const float4 n = g.planes32[f];
@@ -817,6 +828,7 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
   // facet axes are exact overlaps: one below kPen - guard already proves "free"
   {
     const float lf = fminf(pd, wave_minf(loc));
+    TCMP_BOX_CLK(2);
     if (lf < P - kExactGuard) {
 #ifdef TCMP_PROF_EXACT
       if (lane == 0) atomicAdd(&g_exact_stats[1], 1ull);
@@ -911,7 +923,10 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
   if (lane == 0) atomicAdd(&g_exact_stats[__ballot(deg) ? 3 : 2], 1ull);
 #endif
   if (__ballot(deg)) return __builtin_nanf("");
-  return fminf(pd, wave_minf(loc));
+  const float full = fminf(pd, wave_minf(loc));
+  TCMP_BOX_CLK(3);
+  return full;
+#undef TCMP_BOX_CLK
 }
 
 }  // namespace tcmp

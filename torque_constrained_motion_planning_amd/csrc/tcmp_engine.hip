@@ -445,17 +445,24 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 #endif
     // torque test (panda_primitives.py:155-193) -- independent of the collision result, so
     // its order against the collision check does not matter (rrt_star.py:93-96)
+#ifndef TCMP_DIAG_NOTORQUE
     if (active && !lim && P.torque_mode != TCMP_TORQUE_BASE) {
       const double z[7] = {0, 0, 0, 0, 0, 0, 0};
       tok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
                                              : torque_ok<false>(cq, sq, z, z, P.mass);
     }
+#endif
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_torque += c1 - c0; c0 = c1; }
 #endif
     // lanes already failing (limits or torque) need no obstacle pairs
     // every lane calls it (wave-cooperative); lanes already failing only ride along
+#ifdef TCMP_DIAG_NOCOLL
+    // diagnostic builds only (wrong results): no obstacle check at all
+    const bool coll = lim;
+#else
     const bool coll = collides_wave<MESH>(cq, sq, active && !lim && tok, sc, g, ss) || lim;
+#endif
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
 #endif
@@ -679,6 +686,43 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
   const unsigned long long r = wave_sum_u64(rew), sn = wave_sum_u64((unsigned long long)steps);
   if (lane_id() == 0 && r) atomicAdd(&st->rewires, r);
   if (lane_id() == 0 && sn) atomicAdd(&st->edge_steps, sn);
+}
+
+// ------------------------------------------------------------------------------------------
+// peak microbenchmarks (tcmp_microbench): kMbAcc independent FMA chains per thread (fp64, and
+// packed fp32 = v_pk_fma_f32, the form the spec's 157.3 TF counts), and a float4 HBM copy
+// ------------------------------------------------------------------------------------------
+constexpr int kMbAcc = 16;
+__global__ __launch_bounds__(256) void k_mb_fp64(double* out, int iters) {
+  double acc[kMbAcc];
+  const double x = 1.0 + 1e-9 * threadIdx.x, y = 1e-7;
+#pragma unroll
+  for (int k = 0; k < kMbAcc; ++k) acc[k] = 1.0 + k * 1e-3;
+  for (int i = 0; i < iters; ++i)
+#pragma unroll
+    for (int k = 0; k < kMbAcc; ++k) acc[k] = fma(acc[k], x, -y);
+  double s = 0;
+#pragma unroll
+  for (int k = 0; k < kMbAcc; ++k) s += acc[k];
+  if (s == 12345.678) out[0] = s;  // keeps the chains alive, never true
+}
+__global__ __launch_bounds__(256) void k_mb_fp32(double* out, int iters) {
+  f32x2 acc[kMbAcc];
+  const f32x2 x = {1.0f + 1e-7f * threadIdx.x, 1.0f - 1e-7f * threadIdx.x}, y = {1e-6f, 2e-6f};
+#pragma unroll
+  for (int k = 0; k < kMbAcc; ++k) acc[k] = f32x2{1.0f + k * 1e-3f, 1.0f - k * 1e-3f};
+  for (int i = 0; i < iters; ++i)
+#pragma unroll
+    for (int k = 0; k < kMbAcc; ++k) acc[k] = __builtin_elementwise_fma(acc[k], x, -y);
+  float s = 0;
+#pragma unroll
+  for (int k = 0; k < kMbAcc; ++k) s += acc[k].x + acc[k].y;
+  if (s == 12345.678f) out[0] = s;
+}
+__global__ __launch_bounds__(256) void k_mb_copy(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                 long long n) {
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
+    dst[i] = src[i];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3185,6 +3229,61 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
     if (tau) HIPCHK(hipMemcpyAsync(tau, h->ttau.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   }
   HIPCHK(hipStreamSynchronize(h->stream));
+  return 0;
+}
+
+int tcmp_microbench(tcmp_handle* h, double* out) {
+  if (int rc = set_dev(h)) return rc;
+  if (!out) return fail(-1, "null out");
+  // best of 5 launches each, HIP events on the handle's stream
+  hipEvent_t a, b;
+  HIPCHK(hipEventCreate(&a));
+  HIPCHK(hipEventCreate(&b));
+  auto best_ms = [&](auto launch) -> double {
+    double best = 1e30;
+    for (int r = 0; r < 6; ++r) {
+      (void)hipEventRecord(a, h->stream);
+      launch();
+      (void)hipEventRecord(b, h->stream);
+      (void)hipEventSynchronize(b);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, a, b);
+      if (r > 0) best = std::min(best, (double)ms);  // the first launch warms up
+    }
+    return best;
+  };
+  int rc = h->s0.ensure(4 * 65536);
+  if (rc) return rc;
+  const int blocks = std::max(1, h->cu_count) * 8, iters = 4096;
+  const double threads = (double)blocks * 256;
+  double ms = best_ms([&] {
+    hipLaunchKernelGGL(k_mb_fp64, dim3(blocks), dim3(256), 0, h->stream, h->s0.p, iters);
+  });
+  out[0] = 2.0 * kMbAcc * iters * threads / (ms * 1e-3) / 1e12;
+  ms = best_ms([&] {
+    hipLaunchKernelGGL(k_mb_fp32, dim3(blocks), dim3(256), 0, h->stream, h->s0.p, iters);
+  });
+  out[1] = 4.0 * kMbAcc * iters * threads / (ms * 1e-3) / 1e12;
+  // HBM: 1 GiB float4 copy (2 GiB moved per launch), far past the caches
+  const size_t n4 = ((size_t)1 << 30) / 16;
+  float4 *src = nullptr, *dst = nullptr;
+  HIPCHK(hipMalloc(&src, n4 * 16));
+  if (hipMalloc(&dst, n4 * 16) != hipSuccess) {
+    (void)hipFree(src);
+    return fail(-2, "microbench: hipMalloc");
+  }
+  (void)hipMemsetAsync(src, 0, n4 * 16, h->stream);
+  ms = best_ms([&] {
+    hipLaunchKernelGGL(k_mb_copy, dim3(std::max(1, h->cu_count) * 32), dim3(256), 0, h->stream,
+                       src, dst, (long long)n4);
+  });
+  out[2] = 2.0 * (double)n4 * 16 / (ms * 1e-3) / 1e9;
+  out[3] = 0.0;
+  (void)hipFree(src);
+  (void)hipFree(dst);
+  (void)hipEventDestroy(a);
+  (void)hipEventDestroy(b);
+  HIPCHK(hipGetLastError());
   return 0;
 }
 
