@@ -45,8 +45,8 @@ int tcmp_version(void);
 int tcmp_synchronize(tcmp_handle* h);
 /* profiling builds (-DTCMP_PROF) only: k_edges clock breakdown accumulated since create
  * (total, work fetch, collision, torque, bookkeeping, tier-4 exact, ...) and exact-test
- * outcome counts and mesh-stage clocks (12..35), the nearest scan's clocks and visit
- * counts (36..43), n <= 44; zeros otherwise. */
+ * outcome counts and mesh-stage clocks (12..35, then 44..51), the nearest scan's clocks and
+ * visit counts (36..43), n <= 52; zeros otherwise. */
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n);
 
 /* Peak microbenchmarks on the handle's device (the spec peaks are re-measured

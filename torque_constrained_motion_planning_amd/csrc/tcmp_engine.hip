@@ -1427,15 +1427,21 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
                      0, h->stream, st, cfg, T_bound, h->nkeys_in.p, h->nvals_in.p, dP, gf, nb);
   HIPCHK(hipGetLastError());
   size_t tb = h->sort_tmp.n;
-  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, h->nkeys_in.p, h->skeys.p,
-                                             h->nvals_in.p, h->svals.p, (size_t)T_bound, 0,
+  // double-buffer form: the sorted keys / values stay in whichever buffer the last digit pass
+  // wrote (the pass count depends only on the size, so a captured round graph stays valid) --
+  // no copy back into fixed output buffers
+  rocprim::double_buffer<unsigned long long> kdb(h->nkeys_in.p, h->skeys.p);
+  rocprim::double_buffer<int> vdb(h->nvals_in.p, h->svals.p);
+  HIPCHK(rocprim::radix_sort_pairs<SortCfg>(h->sort_tmp.p, tb, kdb, vdb, (size_t)T_bound, 0,
                                              kKeyBits, h->stream));
+  unsigned long long* const skeys = kdb.current();
+  const int* const svals = vdb.current();
   // rows in key order, radix-tree cells of <= 64 nodes, their bounds, super-cells
   hipLaunchKernelGGL(k_nn_rows, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream, st,
-                     dP, cfg, h->svals.p, h->stree.p, h->srow.p, T_bound, h->cflag.p, h->sflag.p);
+                     dP, cfg, svals, h->stree.p, h->srow.p, T_bound, h->cflag.p, h->sflag.p);
   HIPCHK(hipGetLastError());
   hipLaunchKernelGGL(k_nn_cut<kNnC>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
-                     &st->n_nodes, (const int*)nullptr, h->skeys.p, h->cflag.p);
+                     &st->n_nodes, (const int*)nullptr, skeys, h->cflag.p);
   HIPCHK(hipGetLastError());
   tb = h->sort_tmp.n;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(h->sort_tmp.p, tb, h->cflag.p, h->cid.p, (int)T_bound,
@@ -1448,7 +1454,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
   const unsigned idx_grid = (unsigned)std::min<long long>(grid_for(T_bound * 64, 256),
                                                           (long long)h->cu_count * 8);
   hipLaunchKernelGGL(k_nn_cell_boxes, dim3(idx_grid), dim3(256), 0, h->stream,
-                     st, h->stree.p, h->cstart.p, h->skeys.p, h->cboxf.p, h->ckey.p);
+                     st, h->stree.p, h->cstart.p, skeys, h->cboxf.p, h->ckey.p);
   HIPCHK(hipGetLastError());
   // super-cells: the same radix-tree cut over the cells' first keys
   hipLaunchKernelGGL(k_nn_cut<kNnS>, dim3(grid_for(T_bound, 256)), dim3(256), 0, h->stream,
@@ -1482,7 +1488,7 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
                                                kKeyBits - h->nn_cand_bits, kKeyBits, h->stream));
   }
   hipLaunchKernelGGL(k_nn_home, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, st,
-                     h->skeys.p, h->ckeys_in.p, h->cperm.p, h->cid.p, h->sid.p, nb, h->chome.p,
+                     skeys, h->ckeys_in.p, h->cperm.p, h->cid.p, h->sid.p, nb, h->chome.p,
                      bcount);
   HIPCHK(hipGetLastError());
   // one wave per candidate at a time; contiguous Morton-sorted runs per wave (k_nn_home
@@ -1592,17 +1598,20 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (int rc = set_dev(h)) return rc;
-  if (!out || n < 0 || n > 44) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 52) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipStreamSynchronize(h->stream));
   // prof[] has 16 entries; 12..35 are the exact-test stats of TCMP_PROF_EXACT builds
   // 36..43 are the nearest scan's clocks and visit counts (prof_nn)
-  for (int i = 0; i < n; ++i) out[i] = i < 16 ? s.prof[i] : i >= 36 ? s.prof_nn[i - 36] : 0;
+  // 44..51 the exact-test stats 24..31
+  for (int i = 0; i < n; ++i)
+    out[i] = i < 16 ? s.prof[i] : (i >= 36 && i < 44) ? s.prof_nn[i - 36] : 0;
 #ifdef TCMP_PROF_EXACT
-  unsigned long long ex[24];
+  unsigned long long ex[32];
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
   for (int i = 0; i < 24 && 12 + i < n && 12 + i < 36; ++i) out[12 + i] = ex[i];
+  for (int i = 24; i < 32 && 20 + i < n; ++i) out[20 + i] = ex[i];
 #endif
   return 0;
 }
