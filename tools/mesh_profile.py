@@ -30,8 +30,7 @@ def main():
                                     "exact_in_collision": c[5] / tot, "sincos": c[6] / tot,
                                     "tiers123_in_collision": c[7] / tot},
                       "sphere_cert": {"collision": c[26], "free": c[27]}, "facet_wave_free": c[35],
-                      "ball_hull_collision": c[44],
-                      "head_stage_clk": {"ball_hull": c[45], "facet_wave": c[46]},
+                      "head_stage_clk": {"facet_wave": c[46]},
                       "mesh_exact": {"outer_box_free": c[16], "outer_lod_free": c[17],
                                      "inner_collision": c[18], "hull_hull_fp64": c[19]},
                       "hull_hull_exits": {"mesh_facets": c[20], "link_facets": c[21],
@@ -39,7 +38,7 @@ def main():
                                           "full_free": c[24], "degenerate": c[25]},
                       "mesh_stage_clk_share": dict(zip(
                           ("outer_box", "outer_lod", "inner_lod", "full_fp32", "fp64"),
-                          (round(x / max(1, sum(c[28:33]) + c[45] + c[46]), 4) for x in c[28:33])))}),
+                          (round(x / max(1, sum(c[28:33]) + c[46]), 4) for x in c[28:33])))}),
           flush=True)
 
 

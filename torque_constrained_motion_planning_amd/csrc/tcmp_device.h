@@ -35,9 +35,6 @@
 #ifndef TCMP_INNER_FIRST
 #define TCMP_INNER_FIRST 1
 #endif
-#ifndef TCMP_BALL_HULL
-#define TCMP_BALL_HULL 1  // ball-vs-full-hull collision certificate at the head of the mesh chain
-#endif
 
 namespace tcmp {
 
@@ -701,6 +698,9 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g,
                                               const float4* __restrict__ balls = nullptr) {
   const int lane = lane_id();
+  // the ball certificate's load first, so its latency hides behind the box-face pass
+  float4 ball = make_float4(0.f, 0.f, 0.f, -1.f);
+  if (balls && lane < TCMP_NSPH) ball = balls[lane];
 #ifdef TCMP_PROF_EXACT
   // box pairs (balls != null): stage clocks in g_exact_stats[16..19] (box faces, balls,
   // facets, edges) -- slots the mesh stages use in mesh scenes
@@ -766,7 +766,7 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
     // fp32, errors far inside the guard, so the decision is the exact test's.
     float x0 = 0.f, x1 = 0.f, x2 = 0.f, v = -INFINITY, sl = -INFINITY;
     if (lane < TCMP_NSPH) {
-      const float4 b = balls[lane];
+      const float4 b = ball;
       const float s0 = b.x - cl[0], s1 = b.y - cl[1], s2 = b.z - cl[2];
       x0 = A[0] * s0 + A[3] * s1 + A[6] * s2;
       x1 = A[1] * s0 + A[4] * s1 + A[7] * s2;
@@ -1016,54 +1016,6 @@ __device__ __forceinline__ float facet_axes_wave(int link, const float R[9], con
   return fminf(o1, o2);
 }
 
-// Ball-vs-full-hull collision certificate, the head of the mesh chain (exact_pair): every
-// inscribed ball of each body (TCMP_NSPH per body, inside its hull) against the OTHER body's
-// full hull.  A ball whose centre c lies inside a convex polytope penetrates it by exactly
-// r + min over the facets of (d - n.c), and penetration depth is monotone under inclusion, so
-// that value bounds the pair's depth from below: "collision" at kPen + guard and above (the
-// reference's -0.04 closest-points threshold, utils.py:2833).  The pairs that reach the chain
-// are mostly colliding ones (the lane-parallel certificates decide most free pairs), and the
-// full hulls prove far more of them than the inner LODs (tools/cert_study.py).  Lanes: ball
-// lane >> 2, facet stride 4 (lane & 3), then a min over the four lanes; fp32, errors of a few
-// 1e-7 m against the 1e-4 guard.  Returns the best lower bound (-inf: no ball centre inside).
-__device__ __forceinline__ float ball_hull_wave(int link, const float R[9], const float p[3],
-                                                int mi, const int* rg, const Scene sc,
-                                                const Geo g) {
-  const int lane = lane_id();
-  const int b = lane >> 2, q = lane & 3;
-  const float4 t = sc.sph[TCMP_NSPH * (TCMP_NLINKS + mi) + b];  // mesh ball (mesh frame)
-  const float4 s = sc.csph[TCMP_NSPH * link + b];               // link ball (link frame)
-  // mesh ball into the link frame, u = R^T (t - p); link ball into the mesh frame, w = R s + p
-  const float dx = t.x - p[0], dy = t.y - p[1], dz = t.z - p[2];
-  const float ux = R[0] * dx + R[3] * dy + R[6] * dz;
-  const float uy = R[1] * dx + R[4] * dy + R[7] * dz;
-  const float uz = R[2] * dx + R[5] * dy + R[8] * dz;
-  const float wx = R[0] * s.x + R[1] * s.y + R[2] * s.z + p[0];
-  const float wy = R[3] * s.x + R[4] * s.y + R[5] * s.z + p[1];
-  const float wz = R[6] * s.x + R[7] * s.y + R[8] * s.z + p[2];
-  float sl = INFINITY, sm = INFINITY;
-  const int f1 = tcmp_geo_plane_off[link + 1];
-#pragma unroll 4
-  for (int f = tcmp_geo_plane_off[link] + q; f < f1; f += 4) {
-    const float4 n = g.planes32[f];
-    sl = fminf(sl, n.w - (n.x * ux + n.y * uy + n.z * uz));
-  }
-  const int m1 = rg[3];
-#pragma unroll 4
-  for (int f = rg[2] + q; f < m1; f += 4) {
-    const float4 n = sc.mp32[f];
-    sm = fminf(sm, n.w - (n.x * wx + n.y * wy + n.z * wz));
-  }
-  // min over the four lanes of a ball (quad_perm DPP: lanes ^1, ^2)
-  sl = fminf(sl, dpp_f<0xB1>(sl));
-  sl = fminf(sl, dpp_f<0x4E>(sl));
-  sm = fminf(sm, dpp_f<0xB1>(sm));
-  sm = fminf(sm, dpp_f<0x4E>(sm));
-  const float vl = sl >= 0.f ? t.w + sl : -INFINITY;
-  const float vm = sm >= 0.f ? s.w + sm : -INFINITY;
-  return wave_maxf(fmaxf(vl, vm));
-}
-
 // Exact penetration depth of one (link, obstacle) pair, wave-cooperative (all lanes, same
 // arguments); only its comparison with kPen is used.  Boxes: the hull-vs-box test.  Meshes:
 // the link hull against the mesh's outer box ("free" below kPen - guard, the mesh lies inside
@@ -1116,19 +1068,6 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
-  if (TCMP_BALL_HULL && rg[19]) {
-    float Rf[9], pf[3];
-    {
-      const Pose PL = pose();
-#pragma unroll
-      for (int k = 0; k < 9; ++k) Rf[k] = (float)PL.R[k];
-#pragma unroll
-      for (int k = 0; k < 3; ++k) pf[k] = (float)PL.p[k];
-    }
-    const float bh = ball_hull_wave(link, Rf, pf, mi, rg, sc, g);
-    TCMP_MESH_CLK(9);
-    if (bh >= P + kExactGuard) { TCMP_MESH_STAT(24); return (double)bh; }
-  }
   if (TCMP_FACET_WAVE && rg[19]) {
     float Rf[9], pf[3];
     {
@@ -1139,7 +1078,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
       for (int k = 0; k < 3; ++k) pf[k] = (float)PL.p[k];
     }
     const float fa = facet_axes_wave(link, Rf, pf, mi, rg, sc, g);
-    TCMP_MESH_CLK(10);
+    TCMP_MESH_CLK(10);  // slot 26
     if (fa < P - kExactGuard) { TCMP_MESH_STAT(23); return (double)fa; }
   }
   float R[9], p[3];
