@@ -433,6 +433,8 @@ class Engine:
     def microbench(self):
         """Measured peaks of this device (tcmp_microbench): fp64 / packed-fp32 vector TFLOP/s
         and HBM GB/s of a 1 GiB device copy."""
+        if not hasattr(self.L, "tcmp_microbench"):
+            raise TcmpError("tcmp_microbench: not in this library build")
         out = np.zeros(4)
         self._check(self.L.tcmp_microbench(self.h, _d(out)))
         return {"fp64_tflops": float(out[0]), "fp32_tflops": float(out[1]),

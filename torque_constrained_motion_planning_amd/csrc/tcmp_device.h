@@ -696,16 +696,13 @@ __device__ unsigned long long g_exact_stats[32];  // [4..7]: mesh pairs (exact_p
 #endif
 __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
                                               const double* __restrict__ ob, const Geo g,
-                                              const float4* __restrict__ balls = nullptr) {
+                                              bool box_pair = false) {
   const int lane = lane_id();
-  // the ball certificate's load first, so its latency hides behind the box-face pass
-  float4 ball = make_float4(0.f, 0.f, 0.f, -1.f);
-  if (balls && lane < TCMP_NSPH) ball = balls[lane];
 #ifdef TCMP_PROF_EXACT
-  // box pairs (balls != null): stage clocks in g_exact_stats[16..19] (box faces, balls,
-  // facets, edges) -- slots the mesh stages use in mesh scenes
+  // box pairs: stage clocks in g_exact_stats[16..19] (box faces, -, facets, edges) -- slots
+  // the mesh stages use in mesh scenes
   unsigned long long tb = clock64();
-#define TCMP_BOX_CLK(i) if (balls) { const unsigned long long t1 = clock64(); \
+#define TCMP_BOX_CLK(i) if (box_pair) { const unsigned long long t1 = clock64(); \
     if (lane == 0) atomicAdd(&g_exact_stats[16 + (i)], t1 - tb); tb = t1; }
 #else
 #define TCMP_BOX_CLK(i)
@@ -754,69 +751,6 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
     if (lane == 0) atomicAdd(&g_exact_stats[0], 1ull);
 #endif
     return pd;
-  }
-  if (balls) {
-    // Inscribed-ball certificates (box obstacles), wave-cooperative: the link's TCMP_NSPH
-    // balls (inside its hull), one per lane, in the box frame x = A^T (s - cl).  A ball whose
-    // centre is inside the box penetrates it by exactly r + min_j (h_j - |x_j|), a lower bound
-    // of the pair's depth (monotone under inclusion): "collision" at kPen + guard and above.
-    // Otherwise the best ball's direction to its closest box point (inside: its nearest
-    // face's inward normal) is a trial axis a, and the hull's support along it (its vertices)
-    // against the box's exact support overlapping by less than kPen - guard proves "free".
-    // fp32, errors far inside the guard, so the decision is the exact test's.
-    float x0 = 0.f, x1 = 0.f, x2 = 0.f, v = -INFINITY, sl = -INFINITY;
-    if (lane < TCMP_NSPH) {
-      const float4 b = ball;
-      const float s0 = b.x - cl[0], s1 = b.y - cl[1], s2 = b.z - cl[2];
-      x0 = A[0] * s0 + A[3] * s1 + A[6] * s2;
-      x1 = A[1] * s0 + A[4] * s1 + A[7] * s2;
-      x2 = A[2] * s0 + A[5] * s1 + A[8] * s2;
-      const float e0 = fabsf(x0) - h[0], e1 = fabsf(x1) - h[1], e2 = fabsf(x2) - h[2];
-      sl = -fmaxf(e0, fmaxf(e1, e2));
-      const float o0 = fmaxf(e0, 0.f), o1 = fmaxf(e1, 0.f), o2 = fmaxf(e2, 0.f);
-      v = sl >= 0.f ? b.w + sl : b.w - __builtin_sqrtf(o0 * o0 + o1 * o1 + o2 * o2);
-    }
-    const float vb = wave_maxf(v);
-    const int L = __builtin_ctzll(__ballot(v == vb));
-    const float bs = __shfl(sl, L);
-    if (bs >= 0.f && vb >= P + kExactGuard) {
-#ifdef TCMP_PROF_EXACT
-      if (lane == 0) atomicAdd(&g_exact_stats[21], 1ull);
-#endif
-      return vb;
-    }
-    x0 = __shfl(x0, L); x1 = __shfl(x1, L); x2 = __shfl(x2, L);
-    float a0, a1, a2;
-    if (bs < 0.f) {
-      a0 = fminf(fmaxf(x0, -h[0]), h[0]) - x0;
-      a1 = fminf(fmaxf(x1, -h[1]), h[1]) - x1;
-      a2 = fminf(fmaxf(x2, -h[2]), h[2]) - x2;
-    } else {
-      const float s0 = h[0] - fabsf(x0), s1 = h[1] - fabsf(x1), s2 = h[2] - fabsf(x2);
-      a0 = (s0 <= s1 && s0 <= s2) ? (x0 < 0.f ? 1.f : -1.f) : 0.f;
-      a1 = (a0 == 0.f && s1 <= s2) ? (x1 < 0.f ? 1.f : -1.f) : 0.f;
-      a2 = (a0 == 0.f && a1 == 0.f) ? (x2 < 0.f ? 1.f : -1.f) : 0.f;
-    }
-    const float l2 = a0 * a0 + a1 * a1 + a2 * a2;
-    if (l2 > 1e-12f) {
-      const float il = rsqrtf(l2);
-      a0 *= il; a1 *= il; a2 *= il;
-      // the axis in the link frame, l = A a; overlap = max_v v.l - cl.l + sum_j h_j |a_j|
-      const float lx = A[0] * a0 + A[1] * a1 + A[2] * a2;
-      const float ly = A[3] * a0 + A[4] * a1 + A[5] * a2;
-      const float lz = A[6] * a0 + A[7] * a1 + A[8] * a2;
-      float hl = -INFINITY;
-      for (int w = v0 + lane; w < v1; w += 64)
-        hl = fmaxf(hl, g.verts32[3 * w] * lx + g.verts32[3 * w + 1] * ly + g.verts32[3 * w + 2] * lz);
-      const float ov = wave_maxf(hl) - (cl[0] * lx + cl[1] * ly + cl[2] * lz) +
-                       h[0] * fabsf(a0) + h[1] * fabsf(a1) + h[2] * fabsf(a2);
-      if (ov < P - kExactGuard) {
-#ifdef TCMP_PROF_EXACT
-        if (lane == 0) atomicAdd(&g_exact_stats[22], 1ull);
-#endif
-        return ov;
-      }
-    }
   }
   TCMP_BOX_CLK(1);
   float loc = INFINITY;
@@ -917,6 +851,7 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
       if (lf < P - kExactGuard) {
 #ifdef TCMP_PROF_EXACT
         if (lane == 0) atomicAdd(&g_exact_stats[2], 1ull);
+        if (lane == 0 && box_pair) atomicAdd(&g_exact_stats[27], 1ull);  // box: early edge exit
 #endif
         return lf;
       }
@@ -927,6 +862,10 @@ __device__ __forceinline__ float exact_pd_wave32(int link, const Pose pose,
 #endif
   if (__ballot(deg)) return __builtin_nanf("");
   const float full = fminf(pd, wave_minf(loc));
+#ifdef TCMP_PROF_EXACT
+  // box pairs through the whole edge pass: collision / free
+  if (lane == 0 && box_pair) atomicAdd(&g_exact_stats[full >= P ? 28 : 29], 1ull);
+#endif
   TCMP_BOX_CLK(3);
   return full;
 #undef TCMP_BOX_CLK
@@ -1052,8 +991,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     return (const double*)slot;
   };
   if (!MESH || mi < 0) {
-    const float pd32 = exact_pd_wave32(link, pose(), ob, g,
-                                       sc.box_cert ? sc.csph + TCMP_NSPH * link : nullptr);
+    const float pd32 = exact_pd_wave32(link, pose(), ob, g, true);
     if (pd32 == pd32 && fabsf(pd32 - (float)kPen) > kExactGuard) return (double)pd32;
     return exact_pd_wave(link, pose_to_lds(), ob, g.verts, g.planes, g.edges);
   }
