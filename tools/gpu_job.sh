@@ -7,6 +7,7 @@
 #   trace[=W]        rocprofv3 --kernel-trace --stats of the same bench command
 #   pmc[=W]          PMC passes FETCH_SIZE / WRITE_SIZE (one run each) over one bench step
 #   sq[=W]           PMC pass of SQ wave / busy counters over one bench step
+#   valu[=W]         PMC pass of the SQ_INSTS_VALU_* / FLOPS counters over one bench step
 #   prof             profiling-build (make prof) clock breakdowns: tools/nn_profile.py and
 #                    tools/edge_profile.py on C3
 #   ab=LIBS          same-box A/B of libtcmp builds (space-separated .so paths): C3 bench lines,
@@ -55,6 +56,12 @@ for st in "$@"; do
         --kernel-trace -d $O/sq_$w -o run --output-format csv \
         -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
         --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
+    valu)
+      w=${arg:-c3}
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 \
+        --kernel-trace -d $O/valu_$w -o run --output-format csv \
+        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
+        --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
     prof)
       P=torque_constrained_motion_planning_amd/libtcmp_prof.so
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err
