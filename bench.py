@@ -298,9 +298,9 @@ def main():
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
     ap.add_argument("--pipeline", type=int, default=1,
-                    help="single-query workloads: engines that take consecutive steps "
-                         "concurrently (step s on engine s mod P, from host threads), so one "
-                         "query's host calls overlap another's kernels; default 1")
+                    help="steps in flight at once: P consecutive steps' queries run concurrently "
+                         "on separate engines from host threads, so one query's host calls and "
+                         "kernel tails overlap another's kernels (not with --shared-tree)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -365,9 +365,8 @@ def main():
     # (handles, one HIP stream each) from host threads -- the C-ABI calls release the GIL and
     # one 1e5-sample query's rounds do not fill the GPU on their own.  Single-query workloads
     # with --pipeline P run P consecutive steps at once the same way (step s on engine s mod P).
-    pipe = max(1, args.pipeline) if (len(queries) == 1 and not shared) else 1
-    n_streams = max(1, min(len(queries), args.streams if args.streams else
-                           (16 if len(queries) > 1 else 1))) if pipe == 1 else pipe
+    pipe = max(1, args.pipeline) if not shared else 1
+    n_streams = max(1, min(len(queries) * pipe, args.streams if args.streams else 16))
     engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
     for e in engines[1:]:
         e.set_self_collision(args.self_collisions)
@@ -435,20 +434,32 @@ def main():
         total_samples = float(comm.allreduce([total_samples], _lib.REDUCE_SUM)[0])
     n_queries_total = W["queries"] if W["queries"] > 1 else (1 if shared else world)
     S = args.steps
-    kernel_ms = {k: sum(x[k] for x in results) / S for k in
+    host_ms = {k: v / S for k, v in HOST_MS.items()}
+    gathered = dict(GATHER)
+    # Per-kernel figures (kernel_ms, the rooflines) need each launch's own duration.  Pipelined
+    # steps overlap two queries' kernels, and an overlapped launch's event time includes its
+    # neighbour's share of the GPU, so with --pipeline they come from as many steps again run
+    # one at a time after the timed region (same workload, fresh seeds).
+    kres = results
+    if pipe > 1 and len(queries) == 1:
+        kres = []
+        for s in range(args.steps):
+            kres += step_group([30_000 + s])
+        barrier()
+    kernel_ms = {k: sum(x[k] for x in kres) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
     if args.verbose and rank == 0:
         print(json.dumps({"per_step": results, "kernel_ms_per_step": kernel_ms}), file=sys.stderr)
-    launches = sum(x["launches_nearest"] for x in results)  # one k_edges launch per round
+    launches = sum(x["launches_nearest"] for x in kres)  # one k_edges launch per round
     # one scan per round, except a one-node first round (nearest = the root, no index)
-    scans = sum(x["launches_nn_scan"] for x in results)
+    scans = sum(x["launches_nn_scan"] for x in kres)
 
     # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
     # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
     # search never touches, so it is reported beside it, not as "achieved".
-    nn_pairs = sum(x["nn_pairs"] for x in results)
-    nn_full = sum(x["nn_full_pairs"] for x in results)
-    nn_ms = sum(x["ms_nn_scan"] for x in results)
+    nn_pairs = sum(x["nn_pairs"] for x in kres)
+    nn_full = sum(x["nn_full_pairs"] for x in kres)
+    nn_ms = sum(x["ms_nn_scan"] for x in kres)
     nn_tf = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     roof_nn = {
         "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, scans),
@@ -462,11 +473,11 @@ def main():
                            NN_FLOP_PER_PAIR * nn_full / (nn_ms * 1e-3) / 1e15 if nn_ms else 0.0)}
     # k_edges: SURVEY 8d per-step work F_fk + F_bp * L * n_obs + F_rne, + F_sat per pair that
     # survives the cull (device counters), fp64 VALU
-    steps = sum(x["edge_steps"] for x in results)
-    sat = sum(x["pairs_sat"] for x in results)
+    steps = sum(x["edge_steps"] for x in kres)
+    sat = sum(x["pairs_sat"] for x in kres)
     f_rne = 0 if mode == _lib.TORQUE_BASE else F_RNE_STATIC
     edge_flop = steps * (F_FK + F_BP * N_LINKS * n_obs_total + f_rne) + F_SAT * sat
-    ed_ms = sum(x["ms_edges"] for x in results)
+    ed_ms = sum(x["ms_edges"] for x in kres)
     ed_tf = edge_flop / (ed_ms * 1e-3) / 1e12 if ed_ms > 0 else 0.0
     roof_ed = {
         "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
@@ -527,9 +538,11 @@ def main():
                                        "+ 176 B per trajectory row, whole job"},
         "measured_peaks": measured,
         "kernel_ms_per_step": kernel_ms,
+        "kernel_timing": ("%d steps run one at a time after the %d pipelined timed steps" % (S, S)
+                          if kres is not results else "the timed steps"),
         # host wall time inside the C-ABI calls (rank 0; the GPU work of a step completes
         # inside plan_finish's first wait, so "finish" holds most of the step)
-        "host_ms_per_step": {k: v / S for k, v in HOST_MS.items()},
+        "host_ms_per_step": host_ms,
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},
@@ -550,8 +563,8 @@ def main():
             line["tree_digest"] = "%016x" % d
             line["tree_nodes"] = int(nn)
         if not shared:
-            line["gather_ok"] = bool(GATHER["ok"])
-            line["gathered"] = {"queries": GATHER["queries"], "rows": GATHER["rows"],
+            line["gather_ok"] = bool(gathered["ok"])
+            line["gathered"] = {"queries": gathered["queries"], "rows": gathered["rows"],
                                 "steps": S}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         obs, pack, goal = queries[0]
@@ -581,7 +594,7 @@ def main():
             max(1, sum(x["n_samples"] for x in alt_res)),
             "note": "SURVEY 8d default batch; the headline line runs batch_per_round %d" % W["batch"]}
         line["config"]["edge_steps_per_sample"] = steps / max(1.0, float(
-            sum(x["n_samples"] for x in results)))
+            sum(x["n_samples"] for x in kres)))
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:

@@ -385,9 +385,6 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
   unsigned long long c_total = 0, c_fetch = 0, c_coll = 0, c_torque = 0, c_tail = 0, c_sincos = 0;
   const unsigned long long c_start = clock64();
 #endif
-  double res[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k) res[k] = P.res[k];
   while (true) {
 #ifdef TCMP_PROF
     unsigned long long c0 = clock64();
@@ -405,7 +402,9 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
         if (my < J.n) {
           e = J.order ? J.order[my] : my;
           const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
-          double q2[7];
+          double q2[7], res[7];  // (re-read per edge: nothing of it stays live in the loop)
+#pragma unroll
+          for (int k = 0; k < 7; ++k) res[k] = Pd->res[k];
           load7(J.from_base + 8 * src, q);
           load7(J.to + 8 * (size_t)e, q2);
           n = num_steps(q, q2, res);
