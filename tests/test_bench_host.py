@@ -1,0 +1,120 @@
+"""bench.py's host orchestration on the CPU: the step loop, --pipeline (steps in flight on
+separate engines, kernel timings from a one-at-a-time pass), the multi-query deal and the JSON
+line's fields, with the engine replaced by a stand-in (scene calls answered by the oracle, plan
+calls returning synthetic results).  The GPU path itself is covered by the -m gpu tests."""
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests", "golden"))
+
+
+class _FakeEngine:
+    """Scene calls from the oracle (gen_fullsize.OracleEngine); plan calls synthetic, with a
+    short sleep so that concurrent steps really overlap in time."""
+    live = 0
+    peak = 0
+    lock = threading.Lock()
+    seeds = []
+
+    def __init__(self, gpu=0):
+        from gen_fullsize import OracleEngine
+        self._o = OracleEngine()
+
+    def __getattr__(self, name):  # set_scene / collides / torque_ok / check_edges
+        return getattr(self._o, name)
+
+    def microbench(self):
+        return {"fp64_tflops": 1.0, "fp32_tflops": 2.0, "hbm_gbs": 3.0}
+
+    def set_self_collision(self, enable):
+        pass
+
+    def plan_begin(self, start, goal, mode, mass, exec_time, max_nodes, max_batch, seed=0):
+        from torque_constrained_motion_planning_amd import _lib
+        self.n = max_nodes - 1
+        with _FakeEngine.lock:
+            _FakeEngine.seeds.append(seed)
+        return _lib.PLAN_OK
+
+    def plan_run(self, n_samples, batch):
+        with _FakeEngine.lock:
+            _FakeEngine.live += 1
+            _FakeEngine.peak = max(_FakeEngine.peak, _FakeEngine.live)
+        time.sleep(0.02)
+        with _FakeEngine.lock:
+            _FakeEngine.live -= 1
+
+    def plan_finish(self):
+        from torque_constrained_motion_planning_amd import _lib
+        r = _lib.PlanResult()
+        r.status, r.goal_found, r.n_samples, r.n_nodes = 0, 1, self.n, self.n // 2
+        r.n_waypoints, r.n_traj, r.edge_steps, r.pairs_sat = 5, 40, 10 * self.n, self.n
+        r.nn_pairs, r.nn_full_pairs, r.snap_sum = 800 * self.n, self.n * self.n, self.n
+        r.ms_nearest, r.ms_nn_scan, r.ms_edges = 5.0, 4.0, 4.5
+        r.launches_nearest, r.launches_nn_scan = 4, 3
+        return r
+
+    def plan_fetch(self, r):
+        K = r.n_traj
+        return dict(waypoints=np.zeros((r.n_waypoints, 7)), q=np.zeros((K, 7)),
+                    qd=np.zeros((K, 7)), qdd=np.zeros((K, 7)), psg=np.zeros(K),
+                    tau=np.zeros((K, 7)))
+
+    def synchronize(self):
+        pass
+
+    def close(self):
+        pass
+
+
+def _run_bench(monkeypatch, capsys, argv):
+    import bench
+    from torque_constrained_motion_planning_amd import _lib
+    monkeypatch.setattr(_lib, "Engine", _FakeEngine)
+    monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    _FakeEngine.live = _FakeEngine.peak = 0
+    _FakeEngine.seeds = []
+    bench.main()
+    return json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("pipe", [1, 2])
+def test_bench_pipelined_single_query_steps(monkeypatch, capsys, pipe):
+    line = _run_bench(monkeypatch, capsys, ["--workload", "c2", "--steps", "4", "--warmup", "1",
+                                            "--pipeline", str(pipe), "--no-cpu-baseline",
+                                            "--no-alt"])
+    assert line["steps"] == 4 and line["value"] > 0
+    assert line["config"]["pipelined_steps"] == pipe
+    assert line["config"]["streams_per_gpu"] == pipe
+    assert _FakeEngine.peak == pipe  # the pipelined steps really ran concurrently
+    # warmup (pipe queries) + 4 timed, + 4 one-at-a-time kernel-timing queries when pipelined
+    n = pipe + 4 + (4 if pipe > 1 else 0)
+    assert len(_FakeEngine.seeds) == n and len(set(_FakeEngine.seeds)) == n
+    assert ("one at a time" in line["kernel_timing"]) == (pipe > 1)
+    # kernel figures per step from the synthetic results: 4.5 ms of edges in 4 launches
+    assert line["kernel_ms_per_step"]["ms_edges"] == pytest.approx(4.5)
+    assert line["roofline"]["avg_launch_ms"] == pytest.approx(
+        4.0 / 3 if line["roofline"]["kernel"] == "k_nearest_wave32" else 4.5 / 4)
+    assert line["stats_last_step"]["status"] == 0
+
+
+def test_bench_multi_query_pipeline(monkeypatch, capsys):
+    line = _run_bench(monkeypatch, capsys, ["--workload", "c4", "--queries", "3", "--steps", "2",
+                                            "--warmup", "1", "--pipeline", "2",
+                                            "--no-cpu-baseline"])
+    assert line["config"]["queries_per_step"] == 3
+    assert line["config"]["streams_per_gpu"] == 6  # 3 queries x 2 steps in flight
+    assert "timed steps" in line["kernel_timing"]
+    # warmup 2 steps x 3 queries + 2 timed steps x 3 queries, every (query, step) seed distinct
+    assert len(_FakeEngine.seeds) == 12 and len(set(_FakeEngine.seeds)) == 12
+    assert line["value"] == pytest.approx(3 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)
