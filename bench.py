@@ -297,10 +297,11 @@ def main():
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
-    ap.add_argument("--pipeline", type=int, default=1,
+    ap.add_argument("--pipeline", type=int, default=2,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
-                         "kernel tails overlap another's kernels (not with --shared-tree)")
+                         "kernel tails overlap another's kernels (not with --shared-tree); "
+                         "--pipeline 1 runs the steps one after another")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
