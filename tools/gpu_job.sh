@@ -41,27 +41,28 @@ for st in "$@"; do
     trace)
       w=${arg:-c3}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$w -o run --output-format csv \
-        -- python3 bench.py $(bench_args $w) --no-cpu-baseline --no-alt > $O/trace_$w.json 2> $O/trace_$w.err ;;
+        -- python3 bench.py $(bench_args $w) --no-cpu-baseline --no-alt > $O/trace_$w.json 2> $O/trace_$w.err
+      python3 tools/trace_split.py $O/trace_$w/run_kernel_trace.csv > $O/trace_split_$w.json ;;
     pmc)
       w=${arg:-c3}; i=0
       for grp in FETCH_SIZE WRITE_SIZE; do
         i=$((i+1))
         timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-trace -d $O/pmc_$w/p$i -o run --output-format csv \
           -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-          --no-cpu-baseline --no-alt > $O/pmc_${w}_p$i.log 2>&1
+          --pipeline 1 --no-cpu-baseline --no-alt > $O/pmc_${w}_p$i.log 2>&1
       done ;;
     sq)
       w=${arg:-c3}
       timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
         --kernel-trace -d $O/sq_$w -o run --output-format csv \
         -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-        --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
+        --pipeline 1 --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
     valu)
       w=${arg:-c3}
       timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 \
         --kernel-trace -d $O/valu_$w -o run --output-format csv \
         -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-        --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
+        --pipeline 1 --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
     prof)
       P=torque_constrained_motion_planning_amd/libtcmp_prof.so
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err
