@@ -98,20 +98,20 @@ def pmc_valu(kernel, workload, peak, counters=("SQ_INSTS_VALU_FLOPS_FP64",)):
 # 32,768), 262,144 for the 1e6 / 1e7-sample ones.
 WORKLOADS = {
     "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=65536,
-               queries=1, scaling="weak",
+               queries=1, scaling="weak", pipeline=8,
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
-               batch=262144, alt_batch=65536, queries=1, scaling="weak",
+               batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=3,
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
-               queries=64, scaling="strong",
+               queries=64, scaling="strong", pipeline=2,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
                     "samples each) per step, sharded round-robin over the GPUs, solved paths "
                     "gathered to rank 0 over RCCL"),
     "c5": dict(boxes=0, meshes=256, mode=_lib.TORQUE_RNE, mass=5.0, samples=10_000_000,
-               batch=262144, queries=1, scaling="strong",
+               batch=262144, queries=1, scaling="strong", pipeline=2,
                text="C5: dense clutter, 256 convex meshes (Panda link hulls scaled 0.5-1.5, "
                     "random poses), 5 kg, rne, 1e7 samples per step split over the GPUs -- "
                     "throughput mode: N independent replica trees of 1e7/N samples on the same "
@@ -297,11 +297,12 @@ def main():
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=None,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
                          "kernel tails overlap another's kernels (not with --shared-tree); "
-                         "--pipeline 1 runs the steps one after another")
+                         "default per workload (c2 8, c3 3, c4 2, c5 2: the best of a one-box "
+                         "sweep); --pipeline 1 runs the steps one after another")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -366,7 +367,8 @@ def main():
     # (handles, one HIP stream each) from host threads -- the C-ABI calls release the GIL and
     # one 1e5-sample query's rounds do not fill the GPU on their own.  Single-query workloads
     # with --pipeline P run P consecutive steps at once the same way (step s on engine s mod P).
-    pipe = max(1, args.pipeline) if not shared else 1
+    pipe = max(1, args.pipeline if args.pipeline is not None else W.get("pipeline", 1)) \
+        if not shared else 1
     n_streams = max(1, min(len(queries) * pipe, args.streams if args.streams else 16))
     engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
     for e in engines[1:]:

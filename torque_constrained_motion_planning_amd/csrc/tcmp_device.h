@@ -32,6 +32,9 @@
 #ifndef TCMP_FACET_WAVE
 #define TCMP_FACET_WAVE 1
 #endif
+#ifndef TCMP_T0_PACKED
+#define TCMP_T0_PACKED 1  // tier 0 as packed-fp32 bound differences (0: the |centre gap| form)
+#endif
 #ifndef TCMP_INNER_FIRST
 #define TCMP_INNER_FIRST 1
 #endif
@@ -1781,6 +1784,19 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       }
     }
     const int n_tier0 = sc.n_obs + ((MESH && sc.self_coll) ? kNumSelfPairs : 0);
+#if TCMP_T0_PACKED
+    // the link AABBs as bounds, three packed pairs per link: (lo x, lo y), (lo z, -hi x),
+    // (-hi y, -hi z); against an obstacle's (hi x, hi y), (hi z, -lo x), (-lo y, -lo z) the six
+    // differences are all negative iff the boxes overlap (three v_pk_add_f32 and a max per link)
+    typedef float t0f2 __attribute__((ext_vector_type(2)));
+    t0f2 t0a[10], t0b[10], t0c[10];
+#pragma unroll
+    for (int l = 0; l < 10; ++l) {
+      t0a[l] = t0f2{bc[l][0] - bh[l][0], bc[l][1] - bh[l][1]};
+      t0b[l] = t0f2{bc[l][2] - bh[l][2], -(bc[l][0] + bh[l][0])};
+      t0c[l] = t0f2{-(bc[l][1] + bh[l][1]), -(bc[l][2] + bh[l][2])};
+    }
+#endif
     // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
     bool full = false;
     for (int o = o_res; o < n_tier0 && !full; ++o) {
@@ -1788,11 +1804,23 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       if (o < sc.n_obs) {
         const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
         const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
+#if TCMP_T0_PACKED
+        const t0f2 oA = {oa.x + ob4.x, oa.y + ob4.y};
+        const t0f2 oB = {oa.z + ob4.z, ob4.x - oa.x};
+        const t0f2 oC = {ob4.y - oa.y, ob4.z - oa.z};
+#pragma unroll
+        for (int l = 0; l < 10; ++l) {
+          const t0f2 d1 = t0a[l] - oA, d2 = t0b[l] - oB, d3 = t0c[l] - oC;
+          const float m = fmaxf(fmaxf(fmaxf(d1.x, d1.y), fmaxf(d2.x, d2.y)), fmaxf(d3.x, d3.y));
+          lm |= (__float_as_uint(m) >> 31) << l;  // m < 0: overlap on every axis
+        }
+#else
 #pragma unroll
         for (int l = 0; l < 10; ++l)
           lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
                            (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
                            (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
+#endif
       } else if (MESH) {
         const int q = o - sc.n_obs;
         lm = (unsigned)((smask >> q) & 1ull) << kSelfA[q];
