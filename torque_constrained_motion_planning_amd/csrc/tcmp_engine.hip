@@ -1181,6 +1181,7 @@ struct tcmp_handle {
   long long launches_scan = 0;      // k_nearest_wave32 launches of the open plan
   int edge_blocks = 0;
   int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
+  int edge_wps = 2;    // k_edges' persistent grid, blocks per CU (environment TCMP_EDGE_WPS=1/2)
 
   Geo geo() const {
     return Geo{verts.p, planes.p, edges.p, verts32.p,
@@ -1546,7 +1547,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool re
   // persistent grid bounded by residency (256-thread blocks hold one wave per SIMD each).
   // Above it, lanes refill from the longest-first queue; below it, one edge per lane --
   // halving the lanes of a small round (65,536 edges) would leave half the chip idle.
-  const long long cap = (long long)h->cu_count * std::max(2, TCMP_EDGE_MINW);
+  const long long cap = (long long)h->cu_count * std::max(1, std::min(h->edge_wps, TCMP_EDGE_MINW));
   long long lanes = std::max<long long>(64, J.n);
   long long blocks = (lanes + 255) / 256;
   blocks = std::min(blocks, cap);
@@ -1723,6 +1724,7 @@ int tcmp_create(int device, tcmp_handle** out) {
     const int v = std::max(1, std::min(4, atoi(e)));
     h->edge_split = v >= 4 ? 4 : v >= 2 ? 2 : 1;
   }
+  if (const char* e = getenv("TCMP_EDGE_WPS")) h->edge_wps = std::max(1, std::min(2, atoi(e)));
   if (const char* e = getenv("TCMP_NN_CSORT")) h->nn_cand_count_bits = std::min(16, std::max(0, atoi(e)));
   *out = h;
   return 0;
