@@ -20,6 +20,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -379,16 +380,24 @@ def main():
         pool = ThreadPoolExecutor(n_streams)
 
     def run_jobs(jobs):
-        """jobs: (query index, step) pairs, dealt round-robin over the engines' threads."""
+        """jobs: (query index, step) pairs.  Each engine's thread takes the next job as soon as
+        its last one is done, so P steps stay in flight the whole time (no barrier between
+        groups of steps, no idle GPU while the slowest query of a group finishes)."""
+        nxt = iter(range(len(jobs)))
+        take = threading.Lock()
+
         def lane(k):
             got = []
-            for idx in range(k, len(jobs), n_streams):
+            while True:
+                with take:
+                    idx = next(nxt, None)
+                if idx is None:
+                    return got
                 j, s = jobs[idx]
                 obs, pack, goal = queries[j]
                 got.append((idx, s) + run_query(engines[k], obs, goal, W["samples"], W["batch"],
                                                 step_seed(s) + 7919 * j, mode, mass, meshes=pack,
                                                 shared=comm if shared else None))
-            return got
         return sorted(sum(pool.map(lane, range(n_streams)) if pool else [lane(0)], []),
                       key=lambda x: x[0])
 
@@ -415,8 +424,8 @@ def main():
         return res
 
     log("workload %s ready on rank %d of %d" % (args.workload, rank, world))
-    for w in range(args.warmup):
-        step_group([10_000 + w * pipe + k for k in range(pipe)])
+    if args.warmup:
+        step_group([10_000 + i for i in range(args.warmup * pipe)])
     log("warmup done")
 
     barrier()
@@ -425,8 +434,7 @@ def main():
     GATHER.update(ok=True, queries=0, rows=0)
     t0 = time.perf_counter()
     results = []
-    for s0 in range(0, args.steps, pipe):
-        results += step_group(list(range(s0, min(args.steps, s0 + pipe))))
+    results += step_group(list(range(args.steps)))  # gathers (N > 1) follow, in step order
     barrier()
     dt = time.perf_counter() - t0
     log("timed steps done: %.3f s" % dt)
