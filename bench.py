@@ -103,7 +103,7 @@ WORKLOADS = {
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
-               batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=3,
+               batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=4,
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
@@ -302,7 +302,7 @@ def main():
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
                          "kernel tails overlap another's kernels (not with --shared-tree); "
-                         "default per workload (c2 8, c3 3, c4 2, c5 2: the best of a one-box "
+                         "default per workload (c2 8, c3 4, c4 2, c5 2: the best of a one-box "
                          "sweep); --pipeline 1 runs the steps one after another")
     args = ap.parse_args()
 
