@@ -101,11 +101,14 @@ WORKLOADS = {
     "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=65536,
                queries=1, scaling="weak", pipeline=8,
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
-                    "batched samples per query, one query per GPU per step"),
+                    "batched samples per query, one query per GPU per step (queries_in_flight "
+                    "of them planned concurrently)"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
                batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=4,
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
-                    "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step"),
+                    "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step "
+                    "(queries_in_flight of them planned concurrently; config_single_query = one "
+                    "at a time)"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
                queries=64, scaling="strong", pipeline=2,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
@@ -167,6 +170,7 @@ def make_query(seed, n_obs=16, mode=_lib.TORQUE_RNE, mass=5.0, engine=None, n_me
 
 
 HOST_MS = {"begin": 0.0, "run": 0.0, "finish": 0.0, "fetch": 0.0}  # host wall time per call
+HOST_MS_LOCK = threading.Lock()  # run_query runs on several pool threads at once
 GATHER = {"ok": True, "queries": 0, "rows": 0}  # rank 0's checks of the timed steps' gathers
 
 
@@ -191,8 +195,9 @@ def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass
     t3 = time.perf_counter()
     out = eng.plan_fetch(r) if r.goal_found else None
     t4 = time.perf_counter()
-    for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
-        HOST_MS[k] += (b - a) * 1e3
+    with HOST_MS_LOCK:
+        for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
+            HOST_MS[k] += (b - a) * 1e3
     return r, out
 
 
@@ -378,6 +383,11 @@ def main():
     if n_streams > 1:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(n_streams)
+        # concurrent queries: no per-family event timing (an overlapped launch's span includes
+        # its neighbours' kernels, and the round graphs then hold kernel nodes only); the
+        # per-kernel figures come from the one-at-a-time pass after the timed region
+        for e in engines:
+            e.set_timing(False)
 
     def run_jobs(jobs):
         """jobs: (query index, step) pairs.  Each engine's thread takes the next job as soon as
@@ -447,15 +457,34 @@ def main():
     S = args.steps
     host_ms = {k: v / S for k, v in HOST_MS.items()}
     gathered = dict(GATHER)
-    # Per-kernel figures (kernel_ms, the rooflines) need each launch's own duration.  Pipelined
-    # steps overlap two queries' kernels, and an overlapped launch's event time includes its
-    # neighbour's share of the GPU, so with --pipeline they come from as many steps again run
-    # one at a time after the timed region (same workload, fresh seeds).
+    # Per-kernel figures (kernel_ms, the rooflines) need each launch's own duration.  With
+    # queries in flight the engines ran without event timing (an overlapped launch's span would
+    # include its neighbour's share of the GPU), so they come from as many queries again, run
+    # one at a time on one engine after the timed region (same workload, fresh seeds, the
+    # engine's graph captured first); for a single-query workload that pass is also the
+    # one-query-at-a-time throughput (config_single_query), same build, same box.
     kres = results
-    if pipe > 1 and len(queries) == 1:
-        kres = []
-        for s in range(args.steps):
-            kres += step_group([30_000 + s])
+    single = None
+    if n_streams > 1:
+        e0 = engines[0]
+        e0.set_timing(True)
+        obs, pack, goal = queries[0]
+        for w in range(max(1, args.warmup) + 1):  # first sight launches directly, then capture
+            run_query(e0, obs, goal, W["samples"], W["batch"], step_seed(30_000 + 100 + w), mode,
+                      mass, meshes=pack)
+        e0.synchronize()
+        t1 = time.perf_counter()
+        kres = [run_query(e0, obs, goal, W["samples"], W["batch"], step_seed(30_000 + s), mode,
+                          mass, meshes=pack)[0].as_dict() for s in range(S)]
+        e0.synchronize()
+        dts = time.perf_counter() - t1
+        if len(queries) == 1:
+            single = {"value": sum(x["n_samples"] for x in kres) / dts * world,
+                      "unit": "samples/s", "ms_per_step": dts / S * 1e3, "steps": S,
+                      "queries_in_flight": 1,
+                      "note": "the same workload one query at a time on one engine per GPU, "
+                              "after the timed region (rank 0's time x ranks); the headline "
+                              "value keeps %d queries in flight" % pipe}
         barrier()
     kernel_ms = {k: sum(x[k] for x in kres) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
@@ -483,23 +512,34 @@ def main():
                            NN_FLOP_PER_PAIR, nn_pairs, scans, nn_full,
                            NN_FLOP_PER_PAIR * nn_full / (nn_ms * 1e-3) / 1e15 if nn_ms else 0.0)}
     # k_edges: SURVEY 8d per-step work F_fk + F_bp * L * n_obs + F_rne, + F_sat per pair that
-    # survives the cull (device counters), fp64 VALU
-    steps = sum(x["edge_steps"] for x in kres)
+    # survives the cull (device counters).  The steps are k_edges' own: edge_steps less the
+    # rewire edges' (k_rewire_apply, timed under ms_rewire).  Tier 0's F_bp runs in packed
+    # fp32, the rest in fp64, so the bound is the mixed one: the time the fp64 flop need at the
+    # fp64 peak plus the time the fp32 flop need at the fp32 peak; "peak" is the flop rate that
+    # time implies and frac = that time / the measured time.  frac_fp64_contract is the
+    # round-1..4 figure (every flop charged at the fp64 peak).
+    steps = sum(x["edge_steps"] - x.get("rewire_steps", 0) for x in kres)
     sat = sum(x["pairs_sat"] for x in kres)
     f_rne = 0 if mode == _lib.TORQUE_BASE else F_RNE_STATIC
-    edge_flop = steps * (F_FK + F_BP * N_LINKS * n_obs_total + f_rne) + F_SAT * sat
+    flop64 = steps * (F_FK + f_rne) + F_SAT * sat
+    flop32 = steps * F_BP * N_LINKS * n_obs_total
+    edge_flop = flop64 + flop32
+    t_min = flop64 / (PEAK_FP64_TFLOPS * 1e12) + flop32 / (PEAK_FP32_TFLOPS * 1e12)
     ed_ms = sum(x["ms_edges"] for x in kres)
     ed_tf = edge_flop / (ed_ms * 1e-3) / 1e12 if ed_ms > 0 else 0.0
+    peak_mixed = edge_flop / t_min / 1e12 if t_min > 0 else PEAK_FP64_TFLOPS
     roof_ed = {
         "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
-        "bound": "valu_fp64", "achieved": ed_tf, "peak": PEAK_FP64_TFLOPS, "unit": "TFLOP/s",
-        "frac": ed_tf / PEAK_FP64_TFLOPS, "traffic": pmc_traffic("k_edges", args.workload),
+        "bound": "valu_fp64+fp32", "achieved": ed_tf, "peak": peak_mixed, "unit": "TFLOP/s",
+        "frac": ed_tf / peak_mixed, "frac_fp64_contract": ed_tf / PEAK_FP64_TFLOPS,
+        "traffic": pmc_traffic("k_edges", args.workload),
         # the hardware's own count of the kernel's fp64 VALU flop (PMC), beside the SURVEY 8d
         # contract flop above
         "measured_valu": pmc_valu("k_edges", args.workload, PEAK_FP64_TFLOPS),
-        "algorithmic": "per extend step F_fk %d + F_bp %d x %d links x %d obstacles + F_rne %d, "
-                       "+ F_sat %d per pair past the cull; %d steps, %d such pairs, %d launches" % (
-                           F_FK, F_BP, N_LINKS, n_obs_total, f_rne, F_SAT, steps, sat,
+        "algorithmic": "per extend step F_fk %d + F_rne %d (fp64) + F_bp %d x %d links x %d "
+                       "obstacles (packed fp32), + F_sat %d per pair past the cull (fp64); %d "
+                       "k_edges steps (rewire steps excluded), %d such pairs, %d launches" % (
+                           F_FK, f_rne, F_BP, N_LINKS, n_obs_total, F_SAT, steps, sat,
                            launches)}
     for roof, peak in ((roof_nn, PEAK_FP32_TFLOPS), (roof_ed, PEAK_FP64_TFLOPS)):
         mv = roof["measured_valu"]
@@ -507,6 +547,14 @@ def main():
             # the PMC flop per launch over this run's event-timed average launch
             mv["tflops_live"] = mv["flop_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
             mv["frac_live"] = mv["tflops_live"] / peak
+    mv32 = pmc_valu("k_edges", args.workload, PEAK_FP32_TFLOPS, ("SQ_INSTS_VALU_FLOPS_FP32",))
+    mv = roof_ed["measured_valu"]
+    if mv and mv32 and roof_ed["avg_launch_ms"] > 0:
+        # the hardware's fp64 and fp32 flop against the same mixed bound as "frac"
+        t_hw = mv["flop_per_launch"] / (PEAK_FP64_TFLOPS * 1e12) + \
+            mv32["flop_per_launch"] / (PEAK_FP32_TFLOPS * 1e12)
+        mv["fp32_flop_per_launch"] = mv32["flop_per_launch"]
+        mv["frac_live_mixed"] = t_hw / (roof_ed["avg_launch_ms"] * 1e-3)
     for roof, key in ((roof_nn, "fp32_tflops"), (roof_ed, "fp64_tflops")):
         if measured.get(key):
             roof["peak_measured"] = measured[key]
@@ -539,6 +587,7 @@ def main():
                    "batch_per_round": W["batch"], "execution_time_s": 5.0,
                    "parallelism": ("shared-tree x%d" if shared else "query-sharded x%d") % world,
                    "streams_per_gpu": n_streams, "pipelined_steps": pipe,
+                   "queries_in_flight": min(n_streams, len(queries) * pipe),
                    "self_collisions": bool(args.self_collisions)},
         "roofline": dominant,
         "roofline_other": other,
@@ -549,11 +598,14 @@ def main():
                                        "+ 176 B per trajectory row, whole job"},
         "measured_peaks": measured,
         "kernel_ms_per_step": kernel_ms,
-        "kernel_timing": ("%d steps run one at a time after the %d pipelined timed steps" % (S, S)
+        "kernel_timing": ("%d queries run one at a time on one engine after the timed steps "
+                          "(queries in flight run untimed per kernel)" % S
                           if kres is not results else "the timed steps"),
         # host wall time inside the C-ABI calls (rank 0; the GPU work of a step completes
         # inside plan_finish's first wait, so "finish" holds most of the step)
         "host_ms_per_step": host_ms,
+        "host_ms_note": ("per step, summed over the host threads of the queries in flight"
+                         if n_streams > 1 else "per step"),
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},
@@ -606,11 +658,16 @@ def main():
             "note": "SURVEY 8d default batch; the headline line runs batch_per_round %d" % W["batch"]}
         line["config"]["edge_steps_per_sample"] = steps / max(1.0, float(
             sum(x["n_samples"] for x in kres)))
+    if single is not None:
+        line["config_single_query"] = single
     if rank == 0:
         print(json.dumps(line), flush=True)
     if comm is not None:
         comm.close()
-    eng.close()
+    if pool is not None:
+        pool.shutdown(wait=True)
+    for e in reversed(engines):  # every engine released explicitly, the first one last
+        e.close()
 
 
 if __name__ == "__main__":

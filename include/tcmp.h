@@ -114,6 +114,13 @@ int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh,
  * default, as in the reference planner (SELF_COLLISIONS = False, utils.py:56). */
 int tcmp_set_self_collision(tcmp_handle* h, int32_t enable);
 
+/* per-kernel-family device timing of plans (tcmp_plan_result.ms_*: hipEvents recorded around
+ * each family, event nodes inside captured round graphs).  On by default; off records no
+ * events, so a round graph holds kernel nodes only and ms_* stay 0 (queries run concurrently
+ * on several engines, whose event spans would include each other's kernels anyway).  No
+ * reference counterpart (instrumentation). */
+int tcmp_set_timing(tcmp_handle* h, int32_t enable);
+
 /* ---- batched physics (host arrays in/out) ---------------------------------------------- */
 /* rne(q, qd, qdd) with add_payload(r, m) state made explicit: payload iff payload_mass > 0
  * (rne.py:181-254).  q, qd, qdd, tau: n x 7. */
@@ -222,6 +229,8 @@ typedef struct {
   int64_t launches_nn_scan; /* k_nearest_wave32 launches (a one-node first round needs none) */
   uint64_t n_rewires;     /* new.rewire(n, d, path[:-1]) calls (rrt_star.py:187-192) on this
                              engine's lanes */
+  uint64_t rewire_steps;  /* the rewire edges' extend steps (part of edge_steps, not k_edges') */
+  int64_t graph_launches; /* tcmp_plan_run calls of this plan replayed as one captured graph */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

@@ -37,6 +37,9 @@ class _FakeEngine:
     def set_self_collision(self, enable):
         pass
 
+    def set_timing(self, enable):
+        self.timing = bool(enable)
+
     def plan_begin(self, start, goal, mode, mass, exec_time, max_nodes, max_batch, seed=0):
         from torque_constrained_motion_planning_amd import _lib
         self.n = max_nodes - 1
@@ -97,10 +100,16 @@ def test_bench_pipelined_single_query_steps(monkeypatch, capsys, pipe):
     assert line["config"]["pipelined_steps"] == pipe
     assert line["config"]["streams_per_gpu"] == pipe
     assert _FakeEngine.peak == pipe  # the pipelined steps really ran concurrently
-    # warmup (pipe queries) + 4 timed, + 4 one-at-a-time kernel-timing queries when pipelined
-    n = pipe + 4 + (4 if pipe > 1 else 0)
+    # warmup (pipe queries) + 4 timed, + (2 warmup + 4) one-at-a-time queries when pipelined
+    n = pipe + 4 + (6 if pipe > 1 else 0)
     assert len(_FakeEngine.seeds) == n and len(set(_FakeEngine.seeds)) == n
     assert ("one at a time" in line["kernel_timing"]) == (pipe > 1)
+    assert line["config"]["queries_in_flight"] == pipe
+    # the one-query-at-a-time figure rides beside the pipelined value
+    assert ("config_single_query" in line) == (pipe > 1)
+    if pipe > 1:
+        sq = line["config_single_query"]
+        assert sq["queries_in_flight"] == 1 and sq["steps"] == 4 and sq["value"] > 0
     # kernel figures per step from the synthetic results: 4.5 ms of edges in 4 launches
     assert line["kernel_ms_per_step"]["ms_edges"] == pytest.approx(4.5)
     assert line["roofline"]["avg_launch_ms"] == pytest.approx(
@@ -114,7 +123,9 @@ def test_bench_multi_query_pipeline(monkeypatch, capsys):
                                             "--no-cpu-baseline"])
     assert line["config"]["queries_per_step"] == 3
     assert line["config"]["streams_per_gpu"] == 6  # 3 queries x 2 steps in flight
-    assert "timed steps" in line["kernel_timing"]
-    # warmup 2 steps x 3 queries + 2 timed steps x 3 queries, every (query, step) seed distinct
-    assert len(_FakeEngine.seeds) == 12 and len(set(_FakeEngine.seeds)) == 12
+    assert "one at a time" in line["kernel_timing"] and "config_single_query" not in line
+    assert line["config"]["queries_in_flight"] == 6
+    # warmup 2 steps x 3 queries + 2 timed steps x 3 queries, + (2 warmup + 2) one-at-a-time
+    # kernel-timing queries; every seed distinct
+    assert len(_FakeEngine.seeds) == 16 and len(set(_FakeEngine.seeds)) == 16
     assert line["value"] == pytest.approx(3 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)

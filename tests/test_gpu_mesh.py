@@ -108,7 +108,13 @@ def test_mesh_pairs_near_threshold(eng):
     assert checked >= 5
 
 
-def test_mesh_edges_vs_oracle(eng):
+@pytest.mark.parametrize("split", [None, 1, 2])
+def test_mesh_edges_vs_oracle(eng, split):
+    """Safe prefixes and last points against the oracle, through each k_edges<true, SPLIT>
+    instantiation (split None: the engine's own choice for 300 edges, four lanes per edge)."""
+    from conftest import engine_with_split
+    if split is not None:
+        eng = engine_with_split(split)
     rng = np.random.default_rng(9)
     ms, pack = mesh_scene(rng, 16, avoid=[START])
     eng.set_scene(np.zeros((0, 15)), pack)
@@ -123,11 +129,20 @@ def test_mesh_edges_vs_oracle(eng):
         assert ns[i] == s and nt[i] == n, (i, ns[i], s, nt[i], n)
         if s:
             assert np.array_equal(last[i], l), i
+    if split is not None:
+        eng.close()
 
 
+@pytest.mark.parametrize("split", [None, 1, 2])
 @pytest.mark.parametrize("batch,n_mesh", [(1, 8), (64, 16), (512, 32)])
-def test_mesh_batched_frontier_vs_oracle(eng, batch, n_mesh):
+def test_mesh_batched_frontier_vs_oracle(eng, batch, n_mesh, split):
+    """Batched mesh trees against the oracle's batched restatement, through each
+    k_edges<true, SPLIT> the engine can pick (the bench's full C5 rounds run SPLIT 1, its last
+    partial round SPLIT 2)."""
+    from conftest import engine_with_split
     from torque_constrained_motion_planning_amd.rrt_star import rrt_star_batched
+    if split is not None:
+        eng = engine_with_split(split)
     rng = np.random.default_rng(300 + batch)
     goal = None
     while goal is None:
@@ -149,3 +164,5 @@ def test_mesh_batched_frontier_vs_oracle(eng, batch, n_mesh):
         assert r.n_waypoints == ref["n_waypoints"]
         assert np.abs(raw["waypoints"] - ref["waypoints"]).max() < 1e-12
         assert np.abs(raw["q"] - ref["q"]).max() < 1e-9
+    if split is not None:
+        eng.close()

@@ -12,6 +12,7 @@
 #                    tools/edge_profile.py on C3
 #   ab=LIBS          same-box A/B of libtcmp builds (space-separated .so paths): C3 bench lines,
 #                    two passes (tools/ab_lib.sh; bench arguments via env:AB_ARGS=...)
+#   c5seeds=B,S,N    tools/c5_fixture_search.py B S N (goal-reaching seeds of the C5 fixture)
 #   env:VAR=V        export VAR=V for the following stages (A/B knobs, TCMP_LIB_PATH=...)
 # Outputs under gpurun_out/TAG/.
 set -e -o pipefail
@@ -69,6 +70,8 @@ for st in "$@"; do
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/edge_profile.py 2 > $O/edge_profile.json 2> $O/edge_profile.err ;;
     ab)
       bash tools/ab_lib.sh $TAG/ab "$arg" ${AB_ARGS:-} ;;
+    c5seeds)
+      timeout -k 10 300 python -u tools/c5_fixture_search.py ${arg//,/ } > $O/c5seeds.jsonl 2> $O/c5seeds.err ;;
     env:*)
       export "${st#env:}" ;;
     *) echo "unknown stage $st" >&2; exit 2 ;;

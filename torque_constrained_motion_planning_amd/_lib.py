@@ -24,7 +24,7 @@ PLAN_OK, PLAN_START_GOAL_COLLISION, PLAN_NO_GOAL, PLAN_VALIDATION_FAILED, PLAN_M
 EXPORTS = [
     "tcmp_create", "tcmp_destroy", "tcmp_last_error", "tcmp_device_count", "tcmp_version",
     "tcmp_synchronize",
-    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_mesh_spheres", "tcmp_set_self_collision", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
+    "tcmp_set_scene", "tcmp_set_meshes", "tcmp_set_mesh_lods", "tcmp_set_mesh_spheres", "tcmp_set_self_collision", "tcmp_set_timing", "tcmp_rne_batch", "tcmp_torque_ok", "tcmp_check_configs",
     "tcmp_check_body", "tcmp_base_pd",
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
@@ -73,6 +73,7 @@ class PlanResult(ctypes.Structure):
         ("nn_box_tests", ctypes.c_uint64), ("ms_nn_scan", ctypes.c_double),
         ("snap_sum", ctypes.c_uint64), ("nn_full_pairs", ctypes.c_uint64),
         ("launches_nn_scan", ctypes.c_int64), ("n_rewires", ctypes.c_uint64),
+        ("rewire_steps", ctypes.c_uint64), ("graph_launches", ctypes.c_int64),
     ]
 
     def as_dict(self):
@@ -109,6 +110,8 @@ def load_library(path=LIB_PATH):
         if hasattr(L, "tcmp_set_mesh_spheres"):  # absent from A/B builds of older sources
             L.tcmp_set_mesh_spheres.argtypes = [vp, _dp, ctypes.c_int32, ctypes.c_int32]
         L.tcmp_set_self_collision.argtypes = [vp, ctypes.c_int32]
+        if hasattr(L, "tcmp_set_timing"):  # absent from A/B builds of older sources
+            L.tcmp_set_timing.argtypes = [vp, ctypes.c_int32]
         L.tcmp_rne_batch.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_double, _dp]
         L.tcmp_torque_ok.argtypes = [vp, _dp, _dp, _dp, ctypes.c_int64, ctypes.c_int32,
                                      ctypes.c_double, _i32p]
@@ -296,6 +299,10 @@ class Engine:
         self._check(self.L.tcmp_torque_ok(self.h, _d(q), _d(qd), _d(qdd), len(q), int(mode),
                                           float(mass), ok.ctypes.data_as(_i32p)))
         return ok.astype(bool)
+
+    def set_timing(self, enable):
+        """Per-family device timing of plans on/off (tcmp_set_timing; on by default)."""
+        self._check(self.L.tcmp_set_timing(self.h, int(bool(enable))))
 
     def set_self_collision(self, enable):
         """Self-collision pairs on/off for every later check (tcmp_set_self_collision)."""

@@ -46,7 +46,80 @@ int fail(int code, const std::string& msg) {
   return code;
 }
 
+// Process-wide dispatch lock.  Every C-ABI entry point that touches a device holds it shared
+// (reentrant per thread: nested entries take it once); a round-graph capture (tcmp_plan_run)
+// holds it exclusively from hipStreamBeginCapture through the graph's instantiation and first
+// launch, so no other engine's thread enqueues, allocates, frees or synchronizes while a graph
+// is captured or instantiated.  Writer-preferring: a waiting capture blocks new entries, so
+// engines kept busy back to back from several threads (bench.py --pipeline, C4) cannot starve
+// it.  Entry points never wait on one another while holding it (only on their own streams).
+class DispatchLock {
+ public:
+  void lock_shared() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_.wait(lk, [&] { return !writer_ && waiting_ == 0; });
+    ++readers_;
+  }
+  void unlock_shared() {
+    std::lock_guard<std::mutex> lk(m_);
+    if (--readers_ == 0) cv_.notify_all();
+  }
+  void lock() {
+    std::unique_lock<std::mutex> lk(m_);
+    ++waiting_;
+    cv_.wait(lk, [&] { return !writer_ && readers_ == 0; });
+    --waiting_;
+    writer_ = true;
+  }
+  void unlock() {
+    std::lock_guard<std::mutex> lk(m_);
+    writer_ = false;
+    cv_.notify_all();
+  }
+
+ private:
+  std::mutex m_;
+  std::condition_variable cv_;
+  int readers_ = 0, waiting_ = 0;
+  bool writer_ = false;
+};
+DispatchLock g_dispatch;
+thread_local int t_entry_depth = 0;
+thread_local bool t_capturing = false;  // DBuf::ensure refuses to allocate while set
+
+struct Entry {
+  Entry() {
+    if (t_entry_depth++ == 0) g_dispatch.lock_shared();
+  }
+  ~Entry() {
+    if (--t_entry_depth == 0) g_dispatch.unlock_shared();
+  }
+  Entry(const Entry&) = delete;
+  Entry& operator=(const Entry&) = delete;
+};
+
+// exclusive for a capture: the thread's shared hold (an Entry is live) is traded for the
+// exclusive one and given back at the end of the scope
+struct CaptureScope {
+  CaptureScope() {
+    g_dispatch.unlock_shared();
+    g_dispatch.lock();
+    t_capturing = true;
+  }
+  ~CaptureScope() {
+    t_capturing = false;
+    g_dispatch.unlock();
+    g_dispatch.lock_shared();
+  }
+  CaptureScope(const CaptureScope&) = delete;
+  CaptureScope& operator=(const CaptureScope&) = delete;
+};
+
 }  // namespace
+
+#define TCMP_ENTER(h)          \
+  Entry tcmp_entry_;           \
+  if (int rc_ = set_dev(h)) return rc_
 
 // error channel shared with tcmp_dist.cpp (same thread-local message)
 namespace tcmp_err {
@@ -74,6 +147,7 @@ struct DevState {
   long long W, ni, K, first_fail;
   unsigned long long edge_steps, pairs_tested, pairs_sat, pairs_exact, nn_pairs, rewires;
   unsigned long long nn_box_tests;
+  unsigned long long rewire_steps;   // the rewire edges' share of edge_steps (k_rewire_apply)
   unsigned long long snap_sum;       // sum over rounds of the snapshot size T_r
   unsigned long long nn_full_pairs;  // sum over rounds of T_r * B_r (brute-force-equivalent)
   long long ins_total;   // accepted edges of the current round (k_ins_scan), this engine's lanes
@@ -684,7 +758,10 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
   }
   const unsigned long long r = wave_sum_u64(rew), sn = wave_sum_u64((unsigned long long)steps);
   if (lane_id() == 0 && r) atomicAdd(&st->rewires, r);
-  if (lane_id() == 0 && sn) atomicAdd(&st->edge_steps, sn);
+  if (lane_id() == 0 && sn) {
+    atomicAdd(&st->edge_steps, sn);
+    atomicAdd(&st->rewire_steps, sn);
+  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1034,6 +1111,9 @@ struct DBuf {
   size_t n = 0;
   int ensure(size_t want) {
     if (want <= n) return 0;
+    // a captured graph must not bake in a buffer freed under it, and hipFree / hipMalloc
+    // synchronize the device: the capture is abandoned and the rounds run directly
+    if (t_capturing) return fail(-2, "buffer growth during a round-graph capture");
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
@@ -1176,6 +1256,11 @@ struct tcmp_handle {
   unsigned long long rg_seen = 0;  // key seen once: captured when it repeats
   bool use_graphs = true;          // TCMP_GRAPHS=0 disables; a failed capture disables
   bool capturing = false;
+  int graph_failures = 0;          // captures abandoned (two: launch directly from then on)
+  long long graph_launches = 0;    // round-graph launches of the open plan
+  // per-family event timing (tcmp_plan_result.ms_*); tcmp_set_timing(h, 0) records no events,
+  // so a captured round graph then holds kernel nodes only
+  bool timing = true;
   double ms[F_COUNT] = {};
   long long launches_nearest = 0;
   long long launches_scan = 0;      // k_nearest_wave32 launches of the open plan
@@ -1235,12 +1320,14 @@ struct tcmp_handle {
     else (void)hipEventRecord(e, stream);
   }
   hipEvent_t mark() {
+    if (!timing) return nullptr;
     hipEvent_t e = capturing ? new_event() : get_event();
     record(e);
     (capturing ? rg.owned : ev_rec).push_back(e);
     return e;
   }
   void span(int fam, hipEvent_t a, hipEvent_t b) {
+    if (!a || !b) return;  // timing off (tcmp_set_timing)
     (capturing ? rg.events : ev_used).push_back(EventPair{a, b, fam});
   }
   void mark_begin(int fam, hipEvent_t* out) {
@@ -1597,7 +1684,7 @@ const char* tcmp_last_error(void) { return g_err.c_str(); }
 int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!out || n < 0 || n > 52) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
@@ -1617,7 +1704,7 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
 }
 
 int tcmp_synchronize(tcmp_handle* h) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   HIPCHK(hipStreamSynchronize(h->stream));
   return 0;
 }
@@ -1629,6 +1716,7 @@ int tcmp_device_count(int* n) {
 }
 
 int tcmp_create(int device, tcmp_handle** out) {
+  Entry entry;
   if (!out) return fail(-1, "null out");
   *out = nullptr;
   int nd = 0;
@@ -1732,6 +1820,7 @@ int tcmp_create(int device, tcmp_handle** out) {
 
 int tcmp_destroy(tcmp_handle* h) {
   if (!h) return 0;
+  Entry entry;
   (void)hipSetDevice(h->device);
   (void)hipStreamSynchronize(h->stream);
   h->verts32.release();
@@ -2076,7 +2165,7 @@ int upload_scene(tcmp_handle* h) {
 extern "C" {
 
 int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n_obs < 0 || (n_obs > 0 && !obb)) return fail(-1, "bad obstacle array");
   if (n_obs + h->n_mesh > kMaxObstacles)
     return fail(-1, "too many obstacles (" + std::to_string(n_obs + h->n_mesh) + " > " +
@@ -2093,7 +2182,7 @@ int tcmp_set_scene(tcmp_handle* h, const double* obb, int32_t n_obs) {
 int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off,
                     const double* planes, const int32_t* plane_off, const int32_t* edges,
                     const int32_t* edge_off, const double* boxes, int32_t n_mesh) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n_mesh < 0) return fail(-1, "bad mesh count");
   if (n_mesh > 0 && (!verts || !vert_off || !planes || !plane_off || !edges || !edge_off || !boxes))
     return fail(-1, "null mesh array");
@@ -2140,7 +2229,7 @@ int tcmp_set_meshes(tcmp_handle* h, const double* verts, const int32_t* vert_off
 
 int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls* outer,
                        int32_t n_mesh) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n_mesh != h->n_mesh) return fail(-1, "LOD count differs from the mesh count");
   if (n_mesh == 0) return 0;
   if (int rc = check_hulls(inner, n_mesh, "inner")) return rc;
@@ -2160,7 +2249,7 @@ int tcmp_set_mesh_lods(tcmp_handle* h, const tcmp_hulls* inner, const tcmp_hulls
 }
 
 int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh, int32_t k) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n_mesh != h->n_mesh) return fail(-1, "sphere count differs from the mesh count");
   if (k != TCMP_NSPH) return fail(-1, "spheres per mesh must be " + std::to_string(TCMP_NSPH));
   if (n_mesh == 0) return 0;
@@ -2187,7 +2276,7 @@ int tcmp_set_mesh_spheres(tcmp_handle* h, const double* spheres, int32_t n_mesh,
 }
 
 int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   const int on = enable ? 1 : 0;
   if (on == h->self_coll) return 0;
   h->self_coll = on;
@@ -2195,9 +2284,15 @@ int tcmp_set_self_collision(tcmp_handle* h, int32_t enable) {
   return upload_scene(h);
 }
 
+int tcmp_set_timing(tcmp_handle* h, int32_t enable) {
+  TCMP_ENTER(h);
+  h->timing = enable != 0;  // part of the round-graph key: a changed setting captures anew
+  return 0;
+}
+
 int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
                    int64_t n, double payload_mass, double* tau) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!q || !qd || !qdd || !tau))) return fail(-1, "bad arguments");
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, q, n);
@@ -2216,7 +2311,7 @@ int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const doub
 
 int tcmp_ik(tcmp_handle* h, const double* poses, const double* free_q7, int64_t n, double* sols,
             int32_t* count) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!poses || !free_q7 || !sols || !count)))
     return fail(-1, "bad arguments");
   if (n == 0) return 0;
@@ -2241,7 +2336,7 @@ int tcmp_ik(tcmp_handle* h, const double* poses, const double* free_q7, int64_t 
 }
 
 int tcmp_fk(tcmp_handle* h, const double* q, int64_t n, double* poses) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!q || !poses))) return fail(-1, "bad arguments");
   if (n == 0) return 0;
   int rc = h->s0.ensure((size_t)n * 7);
@@ -2260,7 +2355,7 @@ int tcmp_fk(tcmp_handle* h, const double* q, int64_t n, double* poses) {
 
 int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
                    int64_t n, int32_t torque_mode, double payload_mass, int32_t* ok) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!q || !ok))) return fail(-1, "bad arguments");
   if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
   if (n == 0) return 0;
@@ -2279,7 +2374,7 @@ int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const doub
 }
 
 int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* collides) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!q || !collides))) return fail(-1, "bad arguments");
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, q, n);
@@ -2325,7 +2420,7 @@ static int launch_base_pd(tcmp_handle* h) {
 }
 
 int tcmp_base_pd(tcmp_handle* h, double* pd, int32_t n) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n != h->n_box + h->n_mesh) return fail(-1, "n must be the scene's boxes + meshes");
   if (n == 0) return 0;
   if (!pd) return fail(-1, "bad arguments");
@@ -2337,7 +2432,7 @@ int tcmp_base_pd(tcmp_handle* h, double* pd, int32_t n) {
 }
 
 int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collides) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || (n > 0 && (!q || !collides))) return fail(-1, "bad arguments");
   if (n == 0) return 0;
   int rc = upload7(h, h->s0, q, n);
@@ -2369,7 +2464,7 @@ int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collide
 int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64_t n,
                      const double* resolutions, int32_t torque_mode, double payload_mass,
                      int32_t* n_safe, int32_t* n_steps, double* last) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || n > INT_MAX || (n > 0 && (!from || !to || !n_safe || !n_steps || !last)))
     return fail(-1, "bad arguments");
   if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
@@ -2401,7 +2496,7 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
 
 int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* samples,
                  int64_t n, const double* weights, int32_t* idx) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (T <= 0 || T > INT_MAX || n < 0 || n > INT_MAX || !tree || (n > 0 && (!samples || !idx)))
     return fail(-1, "bad arguments");
   if (n == 0) return 0;
@@ -2454,7 +2549,7 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
 
 int tcmp_minjerk(tcmp_handle* h, const double* waypoints, int64_t n_wp, int64_t ni, double* q,
                  double* qd, double* qdd) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (ni <= 0) return fail(-1, "Invalid number of intervals chosen (must be greater than 0)");
   if (n_wp < 1 || !waypoints) return fail(-1, "bad arguments");
   const long long K = (n_wp - 1) * ni;
@@ -2480,7 +2575,7 @@ int tcmp_minjerk(tcmp_handle* h, const double* waypoints, int64_t n_wp, int64_t 
 int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const double* qdd,
                        int64_t n, int32_t torque_mode, double payload_mass, int64_t* first_fail,
                        double* tau) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (n < 0 || !first_fail || (n > 0 && (!q || !qd || !qdd))) return fail(-1, "bad arguments");
   if (torque_mode < 0 || torque_mode > 3) return fail(-1, "unknown torque mode");
   *first_fail = -1;
@@ -2512,7 +2607,7 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
 
 // ---- planner ----------------------------------------------------------------------------
 int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!cfg || !result) return fail(-1, "null cfg/result");
   if (cfg->torque_mode < 0 || cfg->torque_mode > 3) return fail(-1, "unknown torque mode");
   if (cfg->max_nodes < 2 || cfg->max_batch < 1) return fail(-1, "bad capacities");
@@ -2565,6 +2660,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   for (double& m : h->ms) m = 0;
   h->launches_nearest = 0;
   h->launches_scan = 0;
+  h->graph_launches = 0;
   // the finish's buffers, sized here so that tcmp_plan_finish needs one host wait: waypoints
   // (bounded by the chain's total n_safe; generous, checked on the device) and trajectory
   // rows K = (W - 1) * floor(exec_time * 1000 / W) < exec_time * 1000 (k_retrace)
@@ -2642,6 +2738,9 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
   mix((unsigned long long)h->edge_split);
   mix((unsigned long long)h->nn_cand_count_bits);
   mix((unsigned long long)h->sort_tmp.n);
+  mix((unsigned long long)h->timing);
+  mix((unsigned long long)h->edge_wps);
+  mix((unsigned long long)h->cu_count);
   for (const void* p : {(const void*)h->cfg.p, (const void*)h->tgt.p, (const void*)h->parent.p,
                         (const void*)h->meta.p, (const void*)h->cand.p, (const void*)h->last.p,
                         (const void*)h->cgoal.p, (const void*)h->nn.p, (const void*)h->nsafe.p,
@@ -2830,7 +2929,7 @@ static int sr_check(tcmp_handle* h, long long n_samples, int batch, int world) {
 }
 int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goal, int32_t nb,
                     int32_t* goal_found) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
   if (nb < 1 || nb > h->max_batch) return fail(-1, "batch size out of range");
   if (h->samples_issued + nb + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
@@ -2997,7 +3096,7 @@ class GroupExchange : public tcmp_dist::RoundExchange {
 }  // namespace
 
 int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_t batch) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!c) return fail(-1, "null comm");
   const int W = tcmp_dist::world(c);
   if (W == 1) return tcmp_plan_run(h, n_samples, batch);
@@ -3007,6 +3106,7 @@ int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_
 }
 
 int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch) {
+  Entry entry;  // the engines' threads below run inside this entry (they take no lock)
   if (!hs || n < 1) return fail(-1, "bad arguments");
   if (n == 1) return tcmp_plan_run(hs[0], n_samples, batch);
   for (int q = 0; q < n; ++q) {
@@ -3047,7 +3147,7 @@ int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
 }
 
 int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!node) return fail(-1, "null node");
   if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
   long long g = -1;
@@ -3067,7 +3167,7 @@ int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost) {
 }
 
 int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
   if (batch < 1 || batch > h->max_batch) return fail(-1, "batch size out of range");
   if (h->samples_issued + n_samples + 1 > h->P.max_nodes) return fail(-3, "tree capacity exceeded");
@@ -3082,11 +3182,23 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
   };
   if (!h->use_graphs || n_samples <= 0) return run_rounds();
   const unsigned long long key = round_graph_key(h, n_samples, batch);
+  auto account = [&]() {
+    h->samples_issued += n_samples;
+    h->launches_nearest += h->rg.rounds;
+    h->launches_scan += h->rg.scans;
+    h->last_nb = (int)(n_samples % batch ? n_samples % batch : batch);
+  };
   if (!(h->rg.exec && h->rg.key == key)) {
     if (h->rg_seen != key) {  // first sight of this shape: launch directly, capture next time
       h->rg_seen = key;
       return run_rounds();
     }
+    // Capture, instantiate and first launch with every other engine's thread held off (the
+    // dispatch lock, exclusive): the round-4 C5 trace aborted with a malformed AQL packet after
+    // two engines had captured their round graphs while the other engine's thread was
+    // dispatching.  Nothing may allocate or free meanwhile (DBuf::ensure
+    // refuses): the graph would bake in a pointer freed under it.
+    CaptureScope excl;
     h->drop_graph();
     const long long issued = h->samples_issued, launches = h->launches_nearest,
                     scans = h->launches_scan;
@@ -3117,23 +3229,29 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
     h->launches_nearest = launches;
     h->launches_scan = scans;
     h->last_nb = last_nb;
-    if (rc) {  // capture unsupported here: launch directly from now on
-      h->use_graphs = false;
+    if (rc) {
+      // abandoned (a buffer had to grow, or capture is unsupported here): these rounds run
+      // directly; the shape is captured again when it repeats, at most twice in all
+      h->rg_seen = 0;
+      if (++h->graph_failures >= 2) h->use_graphs = false;
       return run_rounds();
     }
+    HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
+    account();
+    ++h->graph_launches;
+    for (const auto& p : h->rg.events) h->ev_used.push_back(p);
+    return 0;
   }
   HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
-  h->samples_issued += n_samples;
-  h->launches_nearest += h->rg.rounds;
-  h->launches_scan += h->rg.scans;
-  h->last_nb = (int)(n_samples % batch ? n_samples % batch : batch);
+  account();
+  ++h->graph_launches;
   for (const auto& p : h->rg.events) h->ev_used.push_back(p);
   return 0;
 }
 
 // traj = false: retrace only (tcmp_plan_retrace, a foreign dynam_fn takes the waypoints)
 static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!r) return fail(-1, "null result");
   if (!h->plan_open) return fail(-1, "no open plan");
   memset(r, 0, sizeof(*r));
@@ -3216,6 +3334,8 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   r->snap_sum = s.snap_sum;
   r->nn_full_pairs = s.nn_full_pairs;
   r->n_rewires = s.rewires;
+  r->rewire_steps = s.rewire_steps;
+  r->graph_launches = h->graph_launches;
   return 0;
 }
 
@@ -3225,7 +3345,7 @@ int tcmp_plan_retrace(tcmp_handle* h, tcmp_plan_result* r) { return plan_finish_
 
 int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
                     double* psg, double* tau) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   // the sizes tcmp_plan_finish read (it waited for the plan); no other state read here
   if (h->fin_W == 0) return fail(-1, "no plan to fetch");
   const long long W = (long long)h->fin_W, K = (long long)h->fin_K;
@@ -3243,7 +3363,7 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
 }
 
 int tcmp_microbench(tcmp_handle* h, double* out) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!out) return fail(-1, "null out");
   // best of 5 launches each, HIP events on the handle's stream
   hipEvent_t a, b;
@@ -3298,7 +3418,7 @@ int tcmp_microbench(tcmp_handle* h, double* out) {
 }
 
 int tcmp_plan_digest(tcmp_handle* h, uint64_t* digest, int64_t* n_nodes) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!digest || !n_nodes) return fail(-1, "null argument");
   if (!h->plan_open) return fail(-1, "no open plan");
   if (int rc = h->u0.ensure(1)) return rc;
@@ -3319,7 +3439,7 @@ int tcmp_plan_digest(tcmp_handle* h, uint64_t* digest, int64_t* n_nodes) {
 
 int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32_t* parent,
                    int64_t* n) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!n) return fail(-1, "null n");
   long long nn = 0;
   HIPCHK(hipMemcpyAsync(&nn, &h->st->n_nodes, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
@@ -3343,7 +3463,7 @@ int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32
 
 int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn,
                           double* score, int64_t* snap, int32_t* nb) {
-  if (int rc = set_dev(h)) return rc;
+  TCMP_ENTER(h);
   if (!snap || !nb || cap < 0) return fail(-1, "bad arguments");
   if (!h->plan_open) return fail(-1, "no open plan");
   long long T = 0;
