@@ -8,6 +8,7 @@ seed, samples, status, nodes, goal node, rewires.
     python tools/c5_fixture_search.py 262144 562816 40     # the bench's batch: two full rounds
                                                            # (k_edges<true,1>) + a 38,528-lane
                                                            # round (k_edges<true,2>), 40 seeds
+    python tools/c5_fixture_search.py 262144 562816:824960 16   # several sample counts
 """
 import json
 import os
@@ -20,9 +21,9 @@ from torque_constrained_motion_planning_amd import _lib  # noqa: E402
 eng = _lib.engine(0)
 obs, pack, goal = bench.make_query(1234, n_obs=0, mode=2, mass=5.0, engine=eng, n_mesh=256)
 if len(sys.argv) > 1:
-    batch, samples = int(sys.argv[1]), int(sys.argv[2])
+    batch = int(sys.argv[1])
     n_seeds = int(sys.argv[3]) if len(sys.argv) > 3 else 24
-    plans = [(batch, samples, n_seeds)]
+    plans = [(batch, int(s), n_seeds) for s in sys.argv[2].split(":")]  # samples: a:b:c
 else:
     plans = [(16384, 16384 * 8, 12), (32768, 32768 * 6, 12), (65536, 65536 * 5, 12)]
 for batch, samples, n_seeds in plans:

@@ -20,24 +20,6 @@
 #include "panda_geometry.inc"
 #include "panda_lod.inc"
 #include "panda_spheres.inc"
-// certificate build knobs: the box form of the lane-parallel certificate, the
-// lane-parallel facet trial axes (both measured slower, off) and the wave-cooperative facet
-// trial axes at the head of the mesh chain (on)
-#ifndef TCMP_BOX_CERT
-#define TCMP_BOX_CERT 0
-#endif
-#ifndef TCMP_FACET_AXES
-#define TCMP_FACET_AXES 0
-#endif
-#ifndef TCMP_FACET_WAVE
-#define TCMP_FACET_WAVE 1
-#endif
-#ifndef TCMP_T0_PACKED
-#define TCMP_T0_PACKED 1  // tier 0 as packed-fp32 bound differences (0: the |centre gap| form)
-#endif
-#ifndef TCMP_INNER_FIRST
-#define TCMP_INNER_FIRST 1
-#endif
 
 namespace tcmp {
 
@@ -142,7 +124,6 @@ struct Scene {
   // link vertices [V][3] -- LDS copies in the mesh kernels (stage_lds), else global
   const float4* csph;
   const float* cv32;
-  int box_cert;  // the box certificate (box_cert) on (TCMP_SPHERES=0 turns both off)
   // self-collision pairs (tcmp_set_self_collision): the 10 link hulls are appended to the
   // mesh arrays as meshes n_mesh + j in their own link frames, and their outer-box records
   // follow the obstacles (obs rows n_obs + j, not in tier 0's obstacle loop)
@@ -496,39 +477,27 @@ __device__ __forceinline__ double wave_min(double x) {
   x = fmin(x, dpp_d<0x4E>(x));
   x = fmin(x, dpp_d<0x124>(x));
   x = fmin(x, dpp_d<0x128>(x));
-#ifdef TCMP_RED_READLANE
-  return fmin(fmin(readlane_d(x, 0), readlane_d(x, 16)), fmin(readlane_d(x, 32), readlane_d(x, 48)));
-#else
   x = fmin(x, bc15_d(x));
   x = fmin(x, bc31_d(x));
   return readlane_d(x, 63);
-#endif
 }
 __device__ __forceinline__ double wave_max(double x) {
   x = fmax(x, dpp_d<0xB1>(x));
   x = fmax(x, dpp_d<0x4E>(x));
   x = fmax(x, dpp_d<0x124>(x));
   x = fmax(x, dpp_d<0x128>(x));
-#ifdef TCMP_RED_READLANE
-  return fmax(fmax(readlane_d(x, 0), readlane_d(x, 16)), fmax(readlane_d(x, 32), readlane_d(x, 48)));
-#else
   x = fmax(x, bc15_d(x));
   x = fmax(x, bc31_d(x));
   return readlane_d(x, 63);
-#endif
 }
 __device__ __forceinline__ int wave_min_int(int x) {
   x = min(x, dpp_i<0xB1>(x));
   x = min(x, dpp_i<0x4E>(x));
   x = min(x, dpp_i<0x124>(x));
   x = min(x, dpp_i<0x128>(x));
-#ifdef TCMP_RED_READLANE
-  return min(min(__builtin_amdgcn_readlane(x, 0), __builtin_amdgcn_readlane(x, 16)), min(__builtin_amdgcn_readlane(x, 32), __builtin_amdgcn_readlane(x, 48)));
-#else
   x = min(x, bc15_i(x));
   x = min(x, bc31_i(x));
   return __builtin_amdgcn_readlane(x, 63);
-#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -644,13 +613,9 @@ __device__ __forceinline__ float wave_minf(float x) {
   x = fminf(x, dpp_f<0x4E>(x));
   x = fminf(x, dpp_f<0x124>(x));
   x = fminf(x, dpp_f<0x128>(x));
-#ifdef TCMP_RED_READLANE
-  return fminf(fminf(readlane_f(x, 0), readlane_f(x, 16)), fminf(readlane_f(x, 32), readlane_f(x, 48)));
-#else
   x = fminf(x, bc15_f(x));
   x = fminf(x, bc31_f(x));
   return readlane_f(x, 63);
-#endif
 }
 __device__ __forceinline__ float wave_minf_bc(float x) {
   x = fminf(x, dpp_f<0xB1>(x));
@@ -666,13 +631,9 @@ __device__ __forceinline__ float wave_maxf(float x) {
   x = fmaxf(x, dpp_f<0x4E>(x));
   x = fmaxf(x, dpp_f<0x124>(x));
   x = fmaxf(x, dpp_f<0x128>(x));
-#ifdef TCMP_RED_READLANE
-  return fmaxf(fmaxf(readlane_f(x, 0), readlane_f(x, 16)), fmaxf(readlane_f(x, 32), readlane_f(x, 48)));
-#else
   x = fmaxf(x, bc15_f(x));
   x = fmaxf(x, bc31_f(x));
   return readlane_f(x, 63);
-#endif
 }
 
 // fp32 first pass of exact_pd_wave on the LDS geometry.  Same candidate axes and the same
@@ -1009,7 +970,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
-  if (TCMP_FACET_WAVE && rg[19]) {
+  if (rg[19]) {
     float Rf[9], pf[3];
     {
       const Pose PL = pose();
@@ -1035,7 +996,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   // certificates leave open collide far more often than the rest, and a failing "free" test
   // runs to completion (every axis) while a failing "collision" test exits at its first axis
   // below the threshold: so, with the certificates on, the inner LODs go first.
-  const bool inner_first = TCMP_INNER_FIRST && rg[18] && rg[19];
+  const bool inner_first = rg[18] && rg[19];
   auto inner_lod = [&]() -> float {
     const HullA32 Ai{sc.lodv3[0], sc.lodpl[0], sc.lodei[0], sc.lodev[0], tcmp_lod_in_vert_off[link],
                      tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
@@ -1332,12 +1293,6 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 #ifndef TCMP_SC_UNROLL
 #define TCMP_SC_UNROLL 8  // stream unroll of sphere_cert's LOD / vertex loops
 #endif
-#ifndef TCMP_SPHERE_CERT
-#define TCMP_SPHERE_CERT 1  // 0: no lane-parallel sphere certificates in phase B (A/B builds)
-#endif
-#ifndef TCMP_CERT_INLINE
-#define TCMP_CERT_INLINE __forceinline__
-#endif
 // Lane-parallel certificates for one pending (link, mesh) pair of phase B, ahead of the
 // wave-cooperative exact chain (exact_pair), which handles one pair at a time with the whole
 // wave.  Inscribed spheres of both hulls (Scene::sph, spheres.py / panda_spheres.inc): a sphere
@@ -1349,7 +1304,7 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 // far inside the 1e-4 guard, so the decision is the exact test's.  Returns 0 free,
 // 1 collision, 2 undecided.  Mesh m: rows TCMP_NSPH * (10 + m) of sph, world frame (link
 // meshes of self pairs: their own link frame, as the pose is then).
-__device__ TCMP_CERT_INLINE int sphere_cert(int link, const float R[9], const float p[3], int mi,
+__device__ __forceinline__ int sphere_cert(int link, const float R[9], const float p[3], int mi,
                                             const Scene sc, const Geo g) {
   const float4* LS = sc.csph + TCMP_NSPH * link;               // LDS (mesh kernels)
   const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);  // global
@@ -1433,140 +1388,7 @@ __device__ TCMP_CERT_INLINE int sphere_cert(int link, const float R[9], const fl
     }
     if (hl + (p[0] * ax + p[1] * ay + p[2] * az) - hm < (float)kPen - kExactGuard) return 0;
   }
-#if TCMP_FACET_AXES
-  // More trial axes: the two mesh facets whose outward normals are closest to -a (axis -n:
-  // overlap = max over the link of -n.x, plus d) and the two link facets whose normals are
-  // closest to +a (axis R n: overlap = d + (R n).p - min over the mesh of (R n).y).  On the
-  // pairs the centre axis leaves open, the minimising axis of the exact test is a facet normal
-  // of one of the hulls in most cases (tools/cert_study.py).
-  int m1 = rg[2], m2 = rg[2], k1 = tcmp_geo_plane_off[link], k2 = k1;
-  {
-    float s1 = -INFINITY, s2 = -INFINITY;
-    const int f1 = rg[3];
-#pragma unroll 8
-    for (int f = rg[2]; f < f1; ++f) {
-      const float4 n = sc.mp32[f];
-      const float sc_ = -(n.x * ax + n.y * ay + n.z * az);
-      if (sc_ > s1) { s2 = s1; m2 = m1; s1 = sc_; m1 = f; } else if (sc_ > s2) { s2 = sc_; m2 = f; }
-    }
-    s1 = -INFINITY; s2 = -INFINITY;
-    const int e1 = tcmp_geo_plane_off[link + 1];
-#pragma unroll 8
-    for (int f = k1; f < e1; ++f) {
-      const float4 n = g.planes32[f];
-      const float sc_ = n.x * bx + n.y * by + n.z * bz;
-      if (sc_ > s1) { s2 = s1; k2 = k1; s1 = sc_; k1 = f; } else if (sc_ > s2) { s2 = sc_; k2 = f; }
-    }
-  }
-  const float4 N1 = sc.mp32[m1], N2 = sc.mp32[m2];
-  const float q1x = -(R[0] * N1.x + R[3] * N1.y + R[6] * N1.z);  // -n in the link frame
-  const float q1y = -(R[1] * N1.x + R[4] * N1.y + R[7] * N1.z);
-  const float q1z = -(R[2] * N1.x + R[5] * N1.y + R[8] * N1.z);
-  const float q2x = -(R[0] * N2.x + R[3] * N2.y + R[6] * N2.z);
-  const float q2y = -(R[1] * N2.x + R[4] * N2.y + R[7] * N2.z);
-  const float q2z = -(R[2] * N2.x + R[5] * N2.y + R[8] * N2.z);
-  float h1 = -INFINITY, h2 = -INFINITY;
-  const int v1 = tcmp_geo_vert_off[link + 1];
-#pragma unroll 4
-  for (int v = tcmp_geo_vert_off[link]; v < v1; ++v) {
-    const float x = sc.cv32[3 * v], y = sc.cv32[3 * v + 1], z = sc.cv32[3 * v + 2];
-    h1 = fmaxf(h1, x * q1x + y * q1y + z * q1z);
-    h2 = fmaxf(h2, x * q2x + y * q2y + z * q2z);
-  }
-  const float o1 = h1 - (p[0] * N1.x + p[1] * N1.y + p[2] * N1.z) + N1.w;
-  const float o2 = h2 - (p[0] * N2.x + p[1] * N2.y + p[2] * N2.z) + N2.w;
-  const float4 L1 = g.planes32[k1], L2 = g.planes32[k2];  // link facet normals in the world
-  const float w1x = R[0] * L1.x + R[1] * L1.y + R[2] * L1.z;
-  const float w1y = R[3] * L1.x + R[4] * L1.y + R[5] * L1.z;
-  const float w1z = R[6] * L1.x + R[7] * L1.y + R[8] * L1.z;
-  const float w2x = R[0] * L2.x + R[1] * L2.y + R[2] * L2.z;
-  const float w2y = R[3] * L2.x + R[4] * L2.y + R[5] * L2.z;
-  const float w2z = R[6] * L2.x + R[7] * L2.y + R[8] * L2.z;
-  float g1 = INFINITY, g2 = INFINITY;
-  const int w1 = rg[1];
-#pragma unroll 8
-  for (int w = rg[0]; w < w1; ++w) {
-    const float4 x = sc.mv32[w];
-    g1 = fminf(g1, x.x * w1x + x.y * w1y + x.z * w1z);
-    g2 = fminf(g2, x.x * w2x + x.y * w2y + x.z * w2z);
-  }
-  const float o3 = L1.w + (p[0] * w1x + p[1] * w1y + p[2] * w1z) - g1;
-  const float o4 = L2.w + (p[0] * w2x + p[1] * w2y + p[2] * w2z) - g2;
-  if (fminf(fminf(o1, o2), fminf(o3, o4)) < (float)kPen - kExactGuard) return 0;
-#endif
   return 2;
-}
-
-// Lane-parallel certificates for one pending (link, box) pair of phase B, the box form of
-// sphere_cert.  For each of the link's inscribed balls: its centre in the box frame x, the
-// inside slack min_k (h_k - |x_k|) and, outside, the distance to the box.  A ball whose centre
-// lies inside the box penetrates it by exactly r + slack, a lower bound of the pair's depth
-// ("collision" at kPen + guard and above).  Otherwise the most-overlapping ball's direction to
-// its closest box point (inside: its nearest face's inward normal) is a trial axis: the link
-// hull's support (its vertices) and the box's exact support overlapping by less than
-// kPen - guard prove "free".  fp32, errors far inside the 1e-4 guard.  0 free, 1 collision,
-// 2 undecided.  ob: c(3), B(9, row-major, columns = axes), h(3).
-__device__ TCMP_CERT_INLINE int box_cert(int link, const double Rd[9], const double pd[3],
-                                         const double* ob, const Scene sc, const Geo g) {
-  // everything in the box frame: x = M s + t with M = B^T R, t = B^T (p - c) (fp64, then fp32)
-  float M[9], t[3], h[3];
-  {
-    const double d0 = pd[0] - ob[0], d1 = pd[1] - ob[1], d2 = pd[2] - ob[2];
-#pragma unroll
-    for (int i = 0; i < 3; ++i) {
-      const double b0 = ob[3 + i], b1 = ob[6 + i], b2 = ob[9 + i];
-#pragma unroll
-      for (int j = 0; j < 3; ++j) M[3 * i + j] = (float)(b0 * Rd[j] + b1 * Rd[3 + j] + b2 * Rd[6 + j]);
-      t[i] = (float)(b0 * d0 + b1 * d1 + b2 * d2);
-      h[i] = (float)ob[12 + i];
-    }
-  }
-  const float4* LS = sc.sph + TCMP_NSPH * link;
-  float best = -INFINITY, bx0 = 0.f, bx1 = 0.f, bx2 = 0.f, bs = 0.f;
-  for (int i = 0; i < TCMP_NSPH; ++i) {
-    const float4 s = LS[i];
-    const float x0 = M[0] * s.x + M[1] * s.y + M[2] * s.z + t[0];
-    const float x1 = M[3] * s.x + M[4] * s.y + M[5] * s.z + t[1];
-    const float x2 = M[6] * s.x + M[7] * s.y + M[8] * s.z + t[2];
-    const float e0 = fabsf(x0) - h[0], e1 = fabsf(x1) - h[1], e2 = fabsf(x2) - h[2];
-    const float slack = -fmaxf(e0, fmaxf(e1, e2));
-    const float o0 = fmaxf(e0, 0.f), o1 = fmaxf(e1, 0.f), o2 = fmaxf(e2, 0.f);
-    const float v = slack >= 0.f ? s.w + slack : s.w - __builtin_sqrtf(o0 * o0 + o1 * o1 + o2 * o2);
-    if (v > best) { best = v; bx0 = x0; bx1 = x1; bx2 = x2; bs = slack; }
-  }
-  if (bs >= 0.f && best >= (float)kPen + kExactGuard) return 1;
-#ifdef TCMP_BALL_ONLY
-  return 2;
-#endif
-  // trial axis a (box frame), from the link into the box
-  float a0, a1, a2;
-  if (bs < 0.f) {
-    a0 = fminf(fmaxf(bx0, -h[0]), h[0]) - bx0;
-    a1 = fminf(fmaxf(bx1, -h[1]), h[1]) - bx1;
-    a2 = fminf(fmaxf(bx2, -h[2]), h[2]) - bx2;
-  } else {
-    const float s0 = h[0] - fabsf(bx0), s1 = h[1] - fabsf(bx1), s2 = h[2] - fabsf(bx2);
-    a0 = (s0 <= s1 && s0 <= s2) ? (bx0 < 0.f ? 1.f : -1.f) : 0.f;
-    a1 = (a0 == 0.f && s1 <= s2) ? (bx1 < 0.f ? 1.f : -1.f) : 0.f;
-    a2 = (a0 == 0.f && a1 == 0.f) ? (bx2 < 0.f ? 1.f : -1.f) : 0.f;
-  }
-  const float l2 = a0 * a0 + a1 * a1 + a2 * a2;
-  if (!(l2 > 1e-12f)) return 2;
-  const float il = rsqrtf(l2);
-  a0 *= il; a1 *= il; a2 *= il;
-  // overlap along a: max_v v.(M^T a) + t.a (the link's support, box frame) minus the box's
-  // support on -a, -(h0 |a0| + h1 |a1| + h2 |a2|)
-  const float lx = M[0] * a0 + M[3] * a1 + M[6] * a2;
-  const float ly = M[1] * a0 + M[4] * a1 + M[7] * a2;
-  const float lz = M[2] * a0 + M[5] * a1 + M[8] * a2;
-  float hl = -INFINITY;
-  const int v1 = tcmp_geo_vert_off[link + 1];
-#pragma unroll 4
-  for (int v = tcmp_geo_vert_off[link]; v < v1; ++v)
-    hl = fmaxf(hl, g.verts32[3 * v] * lx + g.verts32[3 * v + 1] * ly + g.verts32[3 * v + 2] * lz);
-  const float ov = hl + t[0] * a0 + t[1] * a1 + t[2] * a2 + h[0] * fabsf(a0) + h[1] * fabsf(a1) +
-                   h[2] * fabsf(a2);
-  return (ov < (float)kPen - kExactGuard) ? 0 : 2;
 }
 
 // MESH = false: a scene without convex meshes (tcmp_set_meshes count 0) -- the mesh tiers
@@ -1646,15 +1468,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         const double* ob = sc.obs + 16 * orow;
         mi = MESH ? obs_mesh(ob) : -1;
         cls = classify_pair(lk, R, p, wc, U, aabb, ob, mi < 0 ? ob + 12 : sc.mib + 16 * mi + 12, sat);
-        // boxes: the lane-parallel ball / trial-axis certificate before the wave-serial exact
-        // test -- measured slower on C3 (its registers cost more than the exact tests it
-        // saves), so a build knob, off
-        if (TCMP_BOX_CERT && cls == 2 && mi < 0 && sc.box_cert) {
-          cls = box_cert(lk, R, p, ob, sc, g);
-#ifdef TCMP_PROF_EXACT
-          if (cls != 2) atomicAdd(&g_exact_stats[cls ? 21 : 22], 1ull);
-#endif
-        }
       }
       if (MESH && __ballot(cls == 2)) {
         // the undecided pairs' poses go to the stash: R / p (fp64) die here instead of living
@@ -1666,7 +1479,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         for (int k = 0; k < 3; ++k) ps[(9 + k) * 64 + lane] = p[k];
         __asm__ volatile("" ::: "memory");
         // lane-parallel sphere certificates before the wave-serial exact chain (fp32 pose)
-        const bool sp = TCMP_SPHERE_CERT && cls == 2 && mi >= 0 && sc.mrange[kMrange * mi + 19] != 0;
+        const bool sp = cls == 2 && mi >= 0 && sc.mrange[kMrange * mi + 19] != 0;
         if (__ballot(sp) && sp) {
           float Rf[9], pf[3];
 #pragma unroll
@@ -1703,13 +1516,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
 #endif
-#ifdef TCMP_DIAG_NOEXACT
-        // diagnostic builds only (wrong results): undecided pairs collide, no exact test
-        const double pd = kPen;
-        (void)ob;
-#else
         const double pd = exact_pair<MESH>(lL, PL, MESH ? stash + 14 * 64 + L : nullptr, ob, sc, g);
-#endif
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif
@@ -1784,7 +1591,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       }
     }
     const int n_tier0 = sc.n_obs + ((MESH && sc.self_coll) ? kNumSelfPairs : 0);
-#if TCMP_T0_PACKED
     // the link AABBs as bounds, three packed pairs per link: (lo x, lo y), (lo z, -hi x),
     // (-hi y, -hi z); against an obstacle's (hi x, hi y), (hi z, -lo x), (-lo y, -lo z) the six
     // differences are all negative iff the boxes overlap (three v_pk_add_f32 and a max per link)
@@ -1796,7 +1602,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       t0b[l] = t0f2{bc[l][2] - bh[l][2], -(bc[l][0] + bh[l][0])};
       t0c[l] = t0f2{-(bc[l][1] + bh[l][1]), -(bc[l][2] + bh[l][2])};
     }
-#endif
     // tier 0, obstacle-major: one LDS broadcast per obstacle serves all ten links
     bool full = false;
     for (int o = o_res; o < n_tier0 && !full; ++o) {
@@ -1804,7 +1609,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       if (o < sc.n_obs) {
         const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
         const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
-#if TCMP_T0_PACKED
         const t0f2 oA = {oa.x + ob4.x, oa.y + ob4.y};
         const t0f2 oB = {oa.z + ob4.z, ob4.x - oa.x};
         const t0f2 oC = {ob4.y - oa.y, ob4.z - oa.z};
@@ -1814,13 +1618,6 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
           const float m = fmaxf(fmaxf(fmaxf(d1.x, d1.y), fmaxf(d2.x, d2.y)), fmaxf(d3.x, d3.y));
           lm |= (__float_as_uint(m) >> 31) << l;  // m < 0: overlap on every axis
         }
-#else
-#pragma unroll
-        for (int l = 0; l < 10; ++l)
-          lm |= (unsigned)((int)(fabsf(bc[l][0] - oa.x) <= bh[l][0] + ob4.x) &
-                           (int)(fabsf(bc[l][1] - oa.y) <= bh[l][1] + ob4.y) &
-                           (int)(fabsf(bc[l][2] - oa.z) <= bh[l][2] + ob4.z)) << l;
-#endif
       } else if (MESH) {
         const int q = o - sc.n_obs;
         lm = (unsigned)((smask >> q) & 1ull) << kSelfA[q];
@@ -1844,18 +1641,8 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         count += (int)__popcll(bm);
       }
     }
-#ifdef TCMP_DIAG_NOPHASEB
-    // diagnostic builds only (wrong results): every queued pair collides, no phase B
-    if (count) {
-      for (int b = 0; b < count; b += 64)
-        if (b + lane < count) atomicOr(cmask, 1ull << (queue[b + lane] & 63u));
-      __builtin_amdgcn_wave_barrier();
-      count = 0;
-    }
-#else
     // one flush call site (a full queue always holds pairs): phase B is inlined once
     if (count) flush();
-#endif
     if (!full) break;
   }
   __builtin_amdgcn_wave_barrier();

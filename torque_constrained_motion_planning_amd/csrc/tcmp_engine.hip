@@ -268,13 +268,7 @@ __device__ __forceinline__ void goal_fix(const PlanParams* __restrict__ Pd, DevS
 constexpr int kKeyBits = TCMP_KEY_BITS;
 // rocprim picks a block-sort + merge-sort chain (~15 launches) below 1M items by default;
 // the Onesweep radix sort (one histogram pass + one launch per 8-bit digit) is faster here
-#ifdef TCMP_SORT_BS
-using OnesweepCfg = rocprim::radix_sort_onesweep_config<
-    rocprim::kernel_config<256, 12>, rocprim::kernel_config<TCMP_SORT_BS, TCMP_SORT_IPT>,
-    TCMP_SORT_RB, rocprim::block_radix_rank_algorithm::match>;
-#else
 using OnesweepCfg = rocprim::default_config;
-#endif
 using SortCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                            OnesweepCfg, 16384>;
 
@@ -518,24 +512,17 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 #endif
     // torque test (panda_primitives.py:155-193) -- independent of the collision result, so
     // its order against the collision check does not matter (rrt_star.py:93-96)
-#ifndef TCMP_DIAG_NOTORQUE
     if (active && !lim && P.torque_mode != TCMP_TORQUE_BASE) {
       const double z[7] = {0, 0, 0, 0, 0, 0, 0};
       tok = P.torque_mode == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, P.mass)
                                              : torque_ok<false>(cq, sq, z, z, P.mass);
     }
-#endif
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_torque += c1 - c0; c0 = c1; }
 #endif
     // lanes already failing (limits or torque) need no obstacle pairs
     // every lane calls it (wave-cooperative); lanes already failing only ride along
-#ifdef TCMP_DIAG_NOCOLL
-    // diagnostic builds only (wrong results): no obstacle check at all
-    const bool coll = lim;
-#else
     const bool coll = collides_wave<MESH>(cq, sq, active && !lim && tok, sc, g, ss) || lim;
-#endif
 #ifdef TCMP_PROF
     { const unsigned long long c1 = clock64(); c_coll += c1 - c0; c0 = c1; }
 #endif
@@ -1297,7 +1284,6 @@ struct tcmp_handle {
     }
     s.geo_ev = reinterpret_cast<const float4*>(geo_ev.p);
     s.sph = reinterpret_cast<const float4*>(sph.p);
-    s.box_cert = use_sph ? 1 : 0;
     s.n_mesh = n_mesh;
     s.self_coll = self_coll;
     return s;
@@ -1370,6 +1356,19 @@ int set_dev(tcmp_handle* h) {
   return 0;
 }
 
+// A host wait on the handle's stream.  It lets go of the dispatch lock while it waits (the
+// thread holds it once, shared, whatever its entry depth), so a round-graph capture on another
+// engine waits only for the other threads' enqueues, never for their queries to finish: with
+// several queries in flight, a capture would otherwise drain the GPU (bench.py --pipeline).
+int sync_stream(tcmp_handle* h) {
+  const bool held = t_entry_depth > 0 && !t_capturing;
+  if (held) g_dispatch.unlock_shared();
+  const hipError_t e = hipStreamSynchronize(h->stream);
+  if (held) g_dispatch.lock_shared();
+  if (e != hipSuccess) return fail(-2, std::string("hipStreamSynchronize: ") + hipGetErrorString(e));
+  return 0;
+}
+
 // host rows of 7 -> device rows of 8
 int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
   int rc = buf.ensure((size_t)n * 8);
@@ -1379,7 +1378,7 @@ int upload7(tcmp_handle* h, DBuf<double>& buf, const double* src, long long n) {
     for (int k = 0; k < 7; ++k) tmp[8 * i + k] = src[7 * i + k];
   HIPCHK(hipMemcpyAsync(buf.p, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -1688,7 +1687,7 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   if (!out || n < 0 || n > 52) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   // prof[] has 16 entries; 12..35 are the exact-test stats of TCMP_PROF_EXACT builds
   // 36..43 are the nearest scan's clocks and visit counts (prof_nn)
   // 44..51 the exact-test stats 24..31
@@ -1705,7 +1704,7 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
 
 int tcmp_synchronize(tcmp_handle* h) {
   TCMP_ENTER(h);
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2001,7 +2000,7 @@ int upload_meshes(tcmp_handle* h) {
   HIPCHK(hipMemcpyAsync(h->mv32.p, v32.data(), v32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mp32.p, p32.data(), p32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->me32.p, e32.data(), e32.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   h->mrange_h = rg;
   if (int rc = upload_lods(h)) return rc;
   return upload_spheres(h);
@@ -2032,7 +2031,7 @@ int upload_spheres(tcmp_handle* h) {
   HIPCHK(hipMemcpyAsync(h->sph.p, a.data(), a.size() * 4, hipMemcpyHostToDevice, h->stream));
   if (nm)
     HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   h->mrange_h = rg;
   return 0;
 }
@@ -2084,7 +2083,7 @@ int upload_lods(tcmp_handle* h) {
     HIPCHK(hipMemcpyAsync(h->lv32[i].p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->lp32[i].p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->le32[i].p, e32.data(), e32.size() * 4, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
+    if (int rc_s = sync_stream(h)) return rc_s;  // host staging buffers go out of scope
     for (int m = 0; m < nm; ++m) {
       // LOD hull m belongs to mesh m (user) or to link mesh h->n_mesh + (m - n_user)
       const int mesh = m < n_user ? m : h->n_mesh + (m - n_user);
@@ -2096,7 +2095,7 @@ int upload_lods(tcmp_handle* h) {
     }
   }
   HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   h->mrange_h = rg;
   return 0;
 }
@@ -2155,7 +2154,7 @@ int upload_scene(tcmp_handle* h) {
                         h->stream));
   HIPCHK(hipMemcpyAsync(h->obs32.p, t32.data(), t32.size() * sizeof(float), hipMemcpyHostToDevice,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   h->n_obs = n;
   return 0;
 }
@@ -2305,7 +2304,7 @@ int tcmp_rne_batch(tcmp_handle* h, const double* q, const double* qd, const doub
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(tau, h->s3.p, (size_t)n * 7 * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2331,7 +2330,7 @@ int tcmp_ik(tcmp_handle* h, const double* poses, const double* free_q7, int64_t 
                         h->stream));
   HIPCHK(hipMemcpyAsync(count, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2349,7 +2348,7 @@ int tcmp_fk(tcmp_handle* h, const double* q, int64_t n, double* poses) {
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(poses, h->s1.p, (size_t)n * 12 * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2369,7 +2368,7 @@ int tcmp_torque_ok(tcmp_handle* h, const double* q, const double* qd, const doub
                      (long long)n, payload_mass, h->i0.p);
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(ok, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2385,7 +2384,7 @@ int tcmp_check_configs(tcmp_handle* h, const double* q, int64_t n, int32_t* coll
   HIPCHK(hipGetLastError());
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2427,7 +2426,7 @@ int tcmp_base_pd(tcmp_handle* h, double* pd, int32_t n) {
   if (int rc = launch_base_pd(h)) return rc;
   HIPCHK(hipMemcpyAsync(pd, h->base_pd.p, (size_t)n * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2457,7 +2456,7 @@ int tcmp_check_body(tcmp_handle* h, const double* q, int64_t n, int32_t* collide
   }
   HIPCHK(hipMemcpyAsync(collides, h->i0.p, (size_t)n * sizeof(int), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2488,7 +2487,7 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
   HIPCHK(hipMemcpyAsync(n_steps, h->i1.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(tmp.data(), h->s2.p, tmp.size() * sizeof(double), hipMemcpyDeviceToHost,
                         h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   for (long long i = 0; i < n; ++i)
     for (int k = 0; k < 7; ++k) last[7 * i + k] = tmp[8 * i + k];
   return 0;
@@ -2537,7 +2536,7 @@ int tcmp_nearest(tcmp_handle* h, const double* tree, int64_t T, const double* sa
                       nullptr);
   if (rc) return rc;
   HIPCHK(hipMemcpyAsync(idx, h->i0.p, n * sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   // the scan's timing events belong to no plan
   h->ev_used.resize(ev_before);
   while (h->ev_rec.size() > rec_before) {
@@ -2568,7 +2567,7 @@ int tcmp_minjerk(tcmp_handle* h, const double* waypoints, int64_t n_wp, int64_t 
   HIPCHK(hipMemcpyAsync(q, h->s1.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(qd, h->s2.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(qdd, h->s3.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2600,7 +2599,7 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
   HIPCHK(hipMemcpyAsync(&ff, h->u0.p, sizeof(ff), hipMemcpyDeviceToHost, h->stream));
   if (tau)
     HIPCHK(hipMemcpyAsync(tau, h->s3.p, n * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   *first_fail = ff == ~0ull ? -1 : (int64_t)ff;
   return 0;
 }
@@ -2709,7 +2708,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   HIPCHK(hipMemcpyAsync(h->st, &pn.st, sizeof(pn.st), hipMemcpyHostToDevice, h->stream));
   pn.P = h->P;
   HIPCHK(hipMemcpyAsync(h->dP, &pn.P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   h->plan_open = true;
   result->n_nodes = 1;
   result->status = (pn.coll[0] || pn.coll[1]) ? TCMP_PLAN_START_GOAL_COLLISION : TCMP_PLAN_OK;
@@ -2798,7 +2797,7 @@ static int round_sample(tcmp_handle* h, const double* samples, const uint8_t* is
     if (is_goal)
       for (int j = 0; j < nb; ++j) g[j] = is_goal[j] ? 1 : 0;
     HIPCHK(hipMemcpyAsync(h->cgoal.p, g.data(), nb, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));  // host staging buffers go out of scope
+    if (int rc_s = sync_stream(h)) return rc_s;  // host staging buffers go out of scope
   } else {
     hipLaunchKernelGGL(k_sample, dim3(grid_for(nb, 256)), dim3(256), 0, h->stream, h->dP, h->st,
                        (long long)h->samples_issued + lo, nb, h->cand.p, h->cgoal.p);
@@ -2915,7 +2914,7 @@ static inline long long sr_lo(long long B, int q, int W) { return B * q / W; }
 // a host-side copy of the tree size, advanced like k_ins_final does
 static int sr_tree_size(tcmp_handle* h, long long* T) {
   HIPCHK(hipMemcpyAsync(T, &h->st->n_nodes, sizeof(*T), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -2937,7 +2936,7 @@ int tcmp_plan_round(tcmp_handle* h, const double* samples, const uint8_t* is_goa
   if (goal_found) {
     long long g = -1;
     HIPCHK(hipMemcpyAsync(&g, &h->st->goal_node, sizeof(g), hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (int rc_s = sync_stream(h)) return rc_s;
     *goal_found = g >= 0;
   }
   return 0;
@@ -2976,7 +2975,7 @@ static int shared_rounds(tcmp_handle* h, tcmp_dist::RoundExchange& X, long long 
     if (int rc = X.min_i64(x64 + 2, 1, h->stream)) return rc;
     hipLaunchKernelGGL(k_sr_take_goal, dim3(1), dim3(1), 0, h->stream, h->st, x);
     if (int rc = round_finish(h, nb)) return rc;
-    HIPCHK(hipStreamSynchronize(h->stream));  // cnt
+    if (int rc_s = sync_stream(h)) return rc_s;  // cnt
     long long all = 0;
     for (long long v : cnt) all += v;
     if (T + all <= h->P.max_nodes) {
@@ -3152,14 +3151,14 @@ int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost) {
   if (!h->plan_open) return fail(-1, "no open plan (tcmp_plan_begin first)");
   long long g = -1;
   HIPCHK(hipMemcpyAsync(&g, &h->st->goal_node, sizeof(g), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   *node = g;
   if (cost) {
     double c = INFINITY;
     if (g >= 0) {
       HIPCHK(hipMemcpyAsync(&c, h->cfg.p + 8 * (size_t)g + 7, sizeof(c), hipMemcpyDeviceToHost,
                             h->stream));
-      HIPCHK(hipStreamSynchronize(h->stream));
+      if (int rc_s = sync_stream(h)) return rc_s;
     }
     *cost = c;
   }
@@ -3277,7 +3276,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   h->mark_end(F_FINISH, e0);
   DevState& s = h->pin->st;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   r->goal_node = s.goal_node;
   if (s.overflow == 1) return fail(-3, "tree capacity exceeded");
   h->fin_W = 0;
@@ -3302,7 +3301,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
       launch_traj();
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
-      HIPCHK(hipStreamSynchronize(h->stream));
+      if (int rc_s = sync_stream(h)) return rc_s;
     }
     r->n_waypoints = s.W;
     r->n_traj = s.status == TCMP_PLAN_MINJERK_ASSERT ? 0 : s.K;
@@ -3358,7 +3357,7 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
     if (psg) HIPCHK(hipMemcpyAsync(psg, h->tpsg.p, K * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     if (tau) HIPCHK(hipMemcpyAsync(tau, h->ttau.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
   }
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 
@@ -3431,7 +3430,7 @@ int tcmp_plan_digest(tcmp_handle* h, uint64_t* digest, int64_t* n_nodes) {
   unsigned long long d = 0;
   HIPCHK(hipMemcpyAsync(&d, h->u0.p, sizeof(d), hipMemcpyDeviceToHost, h->stream));
   HIPCHK(hipMemcpyAsync(&nn, &h->st->n_nodes, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   *digest = d;
   *n_nodes = nn;
   return 0;
@@ -3443,7 +3442,7 @@ int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32
   if (!n) return fail(-1, "null n");
   long long nn = 0;
   HIPCHK(hipMemcpyAsync(&nn, &h->st->n_nodes, sizeof(nn), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   *n = nn;
   const long long m = std::min<long long>(nn, cap);
   if (m <= 0) return 0;
@@ -3452,7 +3451,7 @@ int tcmp_plan_tree(tcmp_handle* h, int64_t cap, double* cfg, double* cost, int32
                         h->stream));
   if (parent)
     HIPCHK(hipMemcpyAsync(parent, h->parent.p, m * sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   for (long long i = 0; i < m; ++i) {
     if (cfg)
       for (int k = 0; k < 7; ++k) cfg[7 * i + k] = tmp[8 * i + k];
@@ -3468,7 +3467,7 @@ int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn
   if (!h->plan_open) return fail(-1, "no open plan");
   long long T = 0;
   HIPCHK(hipMemcpyAsync(&T, &h->st->snap, sizeof(T), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   *snap = T;
   *nb = h->last_nb;
   const long long m = std::min<long long>(cap, h->last_nb);
@@ -3477,14 +3476,14 @@ int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn
     std::vector<double> tmp((size_t)m * 8);
     HIPCHK(hipMemcpyAsync(tmp.data(), h->cand.p, tmp.size() * sizeof(double),
                           hipMemcpyDeviceToHost, h->stream));
-    HIPCHK(hipStreamSynchronize(h->stream));
+    if (int rc_s = sync_stream(h)) return rc_s;
     for (long long i = 0; i < m; ++i)
       for (int k = 0; k < 7; ++k) cand[7 * i + k] = tmp[8 * i + k];
   }
   if (nn) HIPCHK(hipMemcpyAsync(nn, h->nn.p, m * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   if (score)
     HIPCHK(hipMemcpyAsync(score, h->nnscore.p, m * sizeof(double), hipMemcpyDeviceToHost, h->stream));
-  HIPCHK(hipStreamSynchronize(h->stream));
+  if (int rc_s = sync_stream(h)) return rc_s;
   return 0;
 }
 

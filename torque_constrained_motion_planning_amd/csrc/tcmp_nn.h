@@ -6,8 +6,7 @@
 //   1. k_node_keys + radix sort: Morton keys of the snapshot nodes (9 bits per joint
 //      interleaved, the top kKeyBits = 36 kept; rocPRIM Onesweep radix sort).
 //   2. k_nn_rows: in key order, stree [T][8] f64 (q0..q6, original index) and the rows the
-//      scan's first pass reads, srow: [T][8] f32 (q0..q6, 0), or with TCMP_NN_Q16 [T] uint4
-//      (q0..q6 as u16 on the global grid of nn_qstep).
+//      scan's first pass reads, srow: [T][8] f32 (q0..q6, 0).
 //   3. k_nn_cut<kNnC>: the implicit binary radix tree of the sorted keys (Karras 2012: every
 //      internal node's key range from its neighbours' common-prefix lengths) cut into
 //      "cells": the largest radix-tree subtrees holding at most kNnC nodes.  A cell is a
@@ -24,20 +23,8 @@
 constexpr int kNnC = 64;              // max nodes per cell (one per lane)
 constexpr int kNnS = 64;              // cells per super-cell
 
-// TCMP_NN_Q16 (build knob, default 0): the scan's first pass reads 16-bit rows instead of f32
-// rows -- a quarter of the bytes of the fp64 rows instead of a half.  Measured on C3 (same-box
-// A/B, profiles/r3k_*): the scan's HBM fetch 737 -> 220 MiB in the last round of a query,
-// but 4.07 -> 4.33 ms of scan per query (the unpacking's 7 conversions per node cost more than
-// the cache misses they save: the scan is bound by its dependent round trips, not bytes).
-#ifndef TCMP_NN_Q16
-#define TCMP_NN_Q16 0
-#endif
-// The 16-bit rows: coordinate k of a node is stored as g_k = rint((x_k + cm) / qs) clamped to
-// [0, 65535], cm = P.nn_cmax rounded up to f32 (|x| <= cmax), qs = 2 cm / 65534 in f32 --
-// |x_k - (g_k qs - cm)| <= qs / 2 (+ ~1e-11 qs of fp64 rounding in the quotient).  The build
-// (k_nn_rows) and the scan (tcmp_nn32.h) evaluate the same f32 expressions.
-__device__ __forceinline__ float nn_qcm(double cmax) { return __double2float_ru(cmax); }
-__device__ __forceinline__ float nn_qstep(float cm) { return (2.0f * cm) * (1.0f / 65534.0f); }
+// (16-bit first-pass rows, round 3: 3.4x less HBM fetch but a slower scan -- DESIGN.md
+// section 4; dropped.)
 
 __global__ __launch_bounds__(256) void k_nn_rows(DevState* st, const PlanParams* __restrict__ Pd,
                                                  const double* cfg, const int* svals,
@@ -55,20 +42,9 @@ __global__ __launch_bounds__(256) void k_nn_rows(DevState* st, const PlanParams*
   load7(cfg + 8 * (size_t)n, q);
   store7(stree + 8 * p, q);
   stree[8 * p + 7] = (double)n;
-#if TCMP_NN_Q16
-  const float cm = nn_qcm(Pd->nn_cmax);
-  const double rq = 1.0 / (double)nn_qstep(cm);
-  unsigned g[7];
-#pragma unroll
-  for (int k = 0; k < 7; ++k)
-    g[k] = (unsigned)fmin(fmax(rint((q[k] + (double)cm) * rq), 0.0), 65535.0);
-  reinterpret_cast<uint4*>(srow)[p] =
-      make_uint4(g[0] | (g[1] << 16), g[2] | (g[3] << 16), g[4] | (g[5] << 16), g[6]);
-#else
   float4* d32 = reinterpret_cast<float4*>(srow + 8 * p);
   d32[0] = make_float4((float)q[0], (float)q[1], (float)q[2], (float)q[3]);
   d32[1] = make_float4((float)q[4], (float)q[5], (float)q[6], 0.f);
-#endif
 }
 
 // common-prefix length of keys i and j (ties broken by the index), -1 outside [0, T)

@@ -1,5 +1,5 @@
 // tcmp_nn32.h -- k_nearest_wave32: the exact nearest-neighbour scan of tcmp_nn.h with an fp32
-// first pass (the default build; TCMP_NN_Q16 swaps in 16-bit rows, below).  Included by
+// first pass.  Included by
 // tcmp_engine.hip after tcmp_nn.h.
 //
 // Every (candidate, node) pair is first evaluated in fp32 on the f32 rows srow (half the bytes
@@ -14,12 +14,7 @@
 //   D = exact weighted distance, E = e sqrt(sum w):   r32 <= (1 + g) (D + E)^2,  g = 16 u.
 //   Refine iff r32 <= R(m) = (1 + g)(sqrt(m) + E)^2 (rounded up, with slack).
 //
-// TCMP_NN_Q16 builds (tcmp_nn.h: measured slower, kept as a knob) read 16-bit rows instead
-// (g_k = (x_k + cm) / qs rounded, qs = 2 cm / 65534 with cm the f32 coordinate bound) as
-// d_k = fma(g_k, -qs, o_k), o_k = fl(s32_k + cm) once per candidate; each d_k is then within
-// e = 6 u cmax + 0.5000001 qs of the exact difference (s32 and o_k roundings 3 u cmax, the
-// fma's rounding <= u |d| <= 3 u cmax, quantization qs / 2 plus the build quotient's fp64
-// noise), the same model with the larger e.
+// (16-bit first-pass rows were measured in round 3 and dropped: DESIGN.md section 4.)
 //
 // Nodes that are not refined feed the second-smallest distance through the matching lower
 // bound LB(r32) = (sqrt(r32 / (1 + g)) - E)^2, so `second` is a lower bound of the exact value:
@@ -116,12 +111,7 @@ constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
 // holds at most SW) and a round loads all their rows at once: fewer dependent round trips
 // per candidate than one round per super-cell.
 template <bool UW, int SW>
-#ifdef TCMP_NN_WPE
-#define TCMP_NN_WPE_ATTR __attribute__((amdgpu_waves_per_eu(TCMP_NN_WPE)))
-#else
-#define TCMP_NN_WPE_ATTR
-#endif
-__global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
+__global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* srow, const float* cbox,
                                                         const float* sbox, const float* bbox,
@@ -148,20 +138,9 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     w32[k] = (float)w[k];
     wsum += w[k];
   }
-#if TCMP_NN_Q16
-  const float qcm = nn_qcm(P.nn_cmax), qs = nn_qstep(qcm);
-  const double E = (6.0 * kNnU32 * P.nn_cmax + 0.5000001 * (double)qs) *
-                   sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
-#else
   const double E = 4.0 * kNnU32 * P.nn_cmax * sqrt(UW ? 7.0 : wsum) * (1.0 + 1e-6);
-#endif
   const float G = (float)(8.0 * kNnU32 * P.nn_cmax);  // box_lb32's coordinate shift
-  const double ru = UW ? P.radius / sqrt(P.w[0]) : P.radius;
-#ifndef TCMP_NN_RWPAD
-#define TCMP_NN_RWPAD 0  // 1: pad the pruning threshold by the rewire radius (round 1)
-#endif
-  const float E32 = __double2float_ru(E * (1.0 + 1e-9)),
-              ru32 = TCMP_NN_RWPAD ? __double2float_ru(ru) : 0.f;
+  const float E32 = __double2float_ru(E * (1.0 + 1e-9));
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
   unsigned long long pairs = 0, tests = 0;
 #ifdef TCMP_PROF
@@ -226,9 +205,6 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
 #pragma unroll
     for (int k = 0; k < 7; ++k) s[k] = readlane_d(sl[k], ib);
     float s32[7], sh[7], sl32[7];
-#if TCMP_NN_Q16
-    float so[7];
-#endif
 #pragma unroll
     for (int k = 0; k < 7; ++k) {
       // wave-uniform: readfirstlane puts them back in SGPRs (the VALU arithmetic leaves them
@@ -236,9 +212,6 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
       s32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int((float)s[k])));
       sh[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] + G)));
       sl32[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] - G)));
-#if TCMP_NN_Q16
-      so[k] = __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(s32[k] + qcm)));
-#endif
     }
     const int hc = __builtin_amdgcn_readlane(hml, ib);
     const int hcs = __builtin_amdgcn_readlane(hsl, ib), hcn = __builtin_amdgcn_readlane(hnl, ib);
@@ -278,26 +251,11 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     // seven terms stays inside the error model's g = 16 u
     const f32x2 w01 = {w32[0], w32[1]}, w23 = {w32[2], w32[3]}, w45 = {w32[4], w32[5]},
                 w6 = {w32[6], 0.f};
-#if TCMP_NN_Q16
-    // a 16-bit row against the candidate's grid offsets so: d = so - g qs
-    const float nqs = -qs;
-    auto dist32 = [&](const uint4 R) {
-      const float* o = so;
-      const f32x2 n2 = {nqs, nqs};
-      const f32x2 d01 = __builtin_elementwise_fma(
-          f32x2{(float)(R.x & 0xffffu), (float)(R.x >> 16)}, n2, f32x2{o[0], o[1]});
-      const f32x2 d23 = __builtin_elementwise_fma(
-          f32x2{(float)(R.y & 0xffffu), (float)(R.y >> 16)}, n2, f32x2{o[2], o[3]});
-      const f32x2 d45 = __builtin_elementwise_fma(
-          f32x2{(float)(R.z & 0xffffu), (float)(R.z >> 16)}, n2, f32x2{o[4], o[5]});
-      const f32x2 d6 = {fmaf((float)R.w, nqs, o[6]), 0.f};
-#else
     const f32x2 s01 = {s32[0], s32[1]}, s23 = {s32[2], s32[3]}, s45 = {s32[4], s32[5]},
                 s6 = {s32[6], 0.f};
     auto dist32 = [&](const float4 a, const float4 b) {
       const f32x2 d01 = s01 - f32x2{a.x, a.y}, d23 = s23 - f32x2{a.z, a.w},
                   d45 = s45 - f32x2{b.x, b.y}, d6 = s6 - f32x2{b.z, 0.f};
-#endif
       f32x2 acc;
       if (UW) {
         acc = d01 * d01;
@@ -319,18 +277,14 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
       // (each round-to-nearest step is covered by a 1e-6 relative margin, >> 2^-24)
       const float m32 = wave_minf_bc(__double2float_ru(b1));
       const float sm = sqrtf(m32) * 1.000001f;
-      const float t = (sm + ru32) * 1.000001f;
+      const float t = sm * 1.000001f;
       const float tr = (sm + E32) * 1.000001f;
       Rf = tr * tr * kRfac;
       return t * t * 1.000003f;
     };
     // up to SW cells (count 0 = none), all row loads in flight before any use
     auto scanw = [&](const int cs[SW], const int cn[SW]) -> void {
-#if TCMP_NN_Q16
-      uint4 R[SW];
-#else
       float4 A[SW], Bq[SW];
-#endif
       bool val[SW];
 #pragma unroll
       for (int u = 0; u < SW; ++u) {
@@ -338,15 +292,11 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
         const int c0 = __builtin_amdgcn_readfirstlane(cs[u]);
         const int cnt = __builtin_amdgcn_readfirstlane(cn[u]);
         val[u] = lane < cnt;
-#if TCMP_NN_Q16
-        if (val[u]) R[u] = reinterpret_cast<const uint4*>(srow)[(unsigned)c0 + lane];
-#else
         const float4* rp = reinterpret_cast<const float4*>(srow) + 2 * (unsigned)c0;
         if (val[u]) {
           A[u] = rp[2 * lane];
           Bq[u] = rp[2 * lane + 1];
         }
-#endif
         pairs += (unsigned long long)cnt;
       }
       // the SW distances first, then one branch: refinement (r <= Rf) is the rare case
@@ -354,11 +304,7 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
       float rm = INFINITY;
 #pragma unroll
       for (int u = 0; u < SW; ++u) {
-#if TCMP_NN_Q16
-        r[u] = val[u] ? dist32(R[u]) : INFINITY;
-#else
         r[u] = val[u] ? dist32(A[u], Bq[u]) : INFINITY;
-#endif
         rm = fminf(rm, r[u]);
       }
       if (rm <= Rf) {
@@ -494,7 +440,7 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) TCMP_NN_WPE_ATTR void k_nea
     const double sec = wave_min(mine);
     if (lane == 0) {
       nn[lj] = wi == INT_MAX ? 0 : wi;
-      if (second) second[lj] = TCMP_NN_RWPAD ? sec : fmin(sec, (double)thr);
+      if (second) second[lj] = fmin(sec, (double)thr);
       if (score) score[lj] = m;
     }
     NN_TICK(4);
