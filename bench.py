@@ -469,7 +469,7 @@ def main():
         e0 = engines[0]
         e0.set_timing(True)
         obs, pack, goal = queries[0]
-        for w in range(max(1, args.warmup) + 1):  # first sight launches directly, then capture
+        for w in range(max(1, args.warmup)):  # the first query captures the round graph
             run_query(e0, obs, goal, W["samples"], W["batch"], step_seed(30_000 + 100 + w), mode,
                       mass, meshes=pack)
         e0.synchronize()

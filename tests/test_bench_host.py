@@ -100,8 +100,8 @@ def test_bench_pipelined_single_query_steps(monkeypatch, capsys, pipe):
     assert line["config"]["pipelined_steps"] == pipe
     assert line["config"]["streams_per_gpu"] == pipe
     assert _FakeEngine.peak == pipe  # the pipelined steps really ran concurrently
-    # warmup (pipe queries) + 4 timed, + (2 warmup + 4) one-at-a-time queries when pipelined
-    n = pipe + 4 + (6 if pipe > 1 else 0)
+    # warmup (pipe queries) + 4 timed, + (1 warmup + 4) one-at-a-time queries when pipelined
+    n = pipe + 4 + (5 if pipe > 1 else 0)
     assert len(_FakeEngine.seeds) == n and len(set(_FakeEngine.seeds)) == n
     assert ("one at a time" in line["kernel_timing"]) == (pipe > 1)
     assert line["config"]["queries_in_flight"] == pipe
@@ -125,7 +125,7 @@ def test_bench_multi_query_pipeline(monkeypatch, capsys):
     assert line["config"]["streams_per_gpu"] == 6  # 3 queries x 2 steps in flight
     assert "one at a time" in line["kernel_timing"] and "config_single_query" not in line
     assert line["config"]["queries_in_flight"] == 6
-    # warmup 2 steps x 3 queries + 2 timed steps x 3 queries, + (2 warmup + 2) one-at-a-time
+    # warmup 2 steps x 3 queries + 2 timed steps x 3 queries, + (1 warmup + 2) one-at-a-time
     # kernel-timing queries; every seed distinct
-    assert len(_FakeEngine.seeds) == 16 and len(set(_FakeEngine.seeds)) == 16
+    assert len(_FakeEngine.seeds) == 15 and len(set(_FakeEngine.seeds)) == 15
     assert line["value"] == pytest.approx(3 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)

@@ -134,14 +134,17 @@ def _digest(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.mark.parametrize("name", ["c3", "c5"])
+@pytest.mark.parametrize("name", ["c3", "c5", "c5b"])
 def test_bench_query_vs_oracle_fixture(eng, name):
     """The bench's own query at its own size, bit for bit against the oracle's batched
     restatement (tests/golden/fullsize_<name>.npz, made by tests/golden/gen_fullsize.py):
     C3 = bench.py make_query(1234), 16 boxes, 5 kg, rne, 1e6 samples, B = 262,144, seed 1234
     (step 0 of rank 0); C5 = make_query(1234, n_mesh=256), 131,072 samples in eight rounds of
     16,384 (Philox seed 1243, the goal found in a late round: the nearest scan on a mesh tree,
-    insertion across rounds, retrace, min-jerk and validation at C5 scale).  The scene is
+    insertion across rounds, retrace, min-jerk and validation at C5 scale); C5b = the same
+    scene at the bench's B = 262,144, 562,816 samples (two full rounds through
+    k_edges<true,1>'s persistent refill and a 38,528-lane round through k_edges<true,2>, the
+    bench's own kernels; no goal yet, so the tree is what is pinned).  The scene is
     regenerated on the device by bench.make_query and must be the fixture's; then the final
     tree (configs, costs, parents: sha256), counters, waypoints and trajectory rows match."""
     import os

@@ -490,6 +490,17 @@ __device__ __forceinline__ double wave_max(double x) {
   x = fmax(x, bc31_d(x));
   return readlane_d(x, 63);
 }
+// OR over the wave (every lane active), wave-uniform
+__device__ __forceinline__ unsigned wave_or_u32(unsigned x) {
+  int v = (int)x;
+  v |= dpp_i<0xB1>(v);
+  v |= dpp_i<0x4E>(v);
+  v |= dpp_i<0x124>(v);
+  v |= dpp_i<0x128>(v);
+  v |= bc15_i(v);
+  v |= bc31_i(v);
+  return (unsigned)__builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(v, 63));
+}
 __device__ __forceinline__ int wave_min_int(int x) {
   x = min(x, dpp_i<0xB1>(x));
   x = min(x, dpp_i<0x4E>(x));
@@ -1625,12 +1636,16 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       if (!live) lm = 0;
       if (o == o_res) lm &= ~((1u << l_res) - 1u);  // links already queued before a flush
       if (__ballot(lm != 0u) == 0) continue;
+      // only the links some lane queues (usually one or two of the ten): a wave-uniform walk
+      // over the set bits of the wave's OR, instead of a ballot and branch for every link
+      unsigned um = wave_or_u32(lm);
 #pragma unroll 1
-      for (int l = 0; l < 10; ++l) {
+      while (um) {
+        const int l = __builtin_ctz(um);
+        um &= um - 1u;
         const bool m = (lm >> l) & 1u;
         const uint64_t bm = __ballot(m);
-        if (bm == 0) continue;
-        if (count + 64 > kQcap) {
+        if (count + (int)__popcll(bm) > kQcap) {
           o_res = o;
           l_res = l;
           full = true;

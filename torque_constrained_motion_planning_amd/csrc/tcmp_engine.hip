@@ -1240,7 +1240,6 @@ struct tcmp_handle {
   std::vector<hipEvent_t> ev_rec;   // pool events recorded since (returned to the pool there)
   std::vector<hipEvent_t> ev_pool;
   RoundGraph rg;
-  unsigned long long rg_seen = 0;  // key seen once: captured when it repeats
   bool use_graphs = true;          // TCMP_GRAPHS=0 disables; a failed capture disables
   bool capturing = false;
   int graph_failures = 0;          // captures abandoned (two: launch directly from then on)
@@ -3188,58 +3187,56 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
     h->last_nb = (int)(n_samples % batch ? n_samples % batch : batch);
   };
   if (!(h->rg.exec && h->rg.key == key)) {
-    if (h->rg_seen != key) {  // first sight of this shape: launch directly, capture next time
-      h->rg_seen = key;
-      return run_rounds();
-    }
     // Capture, instantiate and first launch with every other engine's thread held off (the
     // dispatch lock, exclusive): the round-4 C5 trace aborted with a malformed AQL packet after
     // two engines had captured their round graphs while the other engine's thread was
     // dispatching.  Nothing may allocate or free meanwhile (DBuf::ensure
     // refuses): the graph would bake in a pointer freed under it.
-    CaptureScope excl;
-    h->drop_graph();
-    const long long issued = h->samples_issued, launches = h->launches_nearest,
-                    scans = h->launches_scan;
-    const int last_nb = h->last_nb;
     int rc = 0;
-    if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
-      rc = -2;
-    } else {
-      h->capturing = true;
-      rc = run_rounds();
-      h->capturing = false;
-      hipGraph_t g = nullptr;
-      const hipError_t e = hipStreamEndCapture(h->stream, &g);
-      if (rc == 0 && e == hipSuccess && g &&
-          hipGraphInstantiate(&h->rg.exec, g, nullptr, nullptr, 0) == hipSuccess) {
-        h->rg.graph = g;
-        h->rg.key = key;
-        h->rg.rounds = (int)(h->launches_nearest - launches);
-        h->rg.scans = (int)(h->launches_scan - scans);
+    {
+      CaptureScope excl;
+      h->drop_graph();
+      const long long issued = h->samples_issued, launches = h->launches_nearest,
+                      scans = h->launches_scan;
+      const int last_nb = h->last_nb;
+      if (hipStreamBeginCapture(h->stream, hipStreamCaptureModeRelaxed) != hipSuccess) {
+        rc = -2;
       } else {
-        if (g) (void)hipGraphDestroy(g);
-        h->drop_graph();
-        rc = rc ? rc : -2;
+        h->capturing = true;
+        rc = run_rounds();
+        h->capturing = false;
+        hipGraph_t g = nullptr;
+        const hipError_t e = hipStreamEndCapture(h->stream, &g);
+        if (rc == 0 && e == hipSuccess && g &&
+            hipGraphInstantiate(&h->rg.exec, g, nullptr, nullptr, 0) == hipSuccess) {
+          h->rg.graph = g;
+          h->rg.key = key;
+          h->rg.rounds = (int)(h->launches_nearest - launches);
+          h->rg.scans = (int)(h->launches_scan - scans);
+        } else {
+          if (g) (void)hipGraphDestroy(g);
+          h->drop_graph();
+          rc = rc ? rc : -2;
+        }
+      }
+      (void)hipGetLastError();
+      h->samples_issued = issued;  // nothing ran yet
+      h->launches_nearest = launches;
+      h->launches_scan = scans;
+      h->last_nb = last_nb;
+      if (!rc) {
+        HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
+        account();
+        ++h->graph_launches;
+        for (const auto& p : h->rg.events) h->ev_used.push_back(p);
+        return 0;
       }
     }
-    (void)hipGetLastError();
-    h->samples_issued = issued;  // nothing ran yet
-    h->launches_nearest = launches;
-    h->launches_scan = scans;
-    h->last_nb = last_nb;
-    if (rc) {
-      // abandoned (a buffer had to grow, or capture is unsupported here): these rounds run
-      // directly; the shape is captured again when it repeats, at most twice in all
-      h->rg_seen = 0;
-      if (++h->graph_failures >= 2) h->use_graphs = false;
-      return run_rounds();
-    }
-    HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
-    account();
-    ++h->graph_launches;
-    for (const auto& p : h->rg.events) h->ev_used.push_back(p);
-    return 0;
+    // abandoned (a buffer had to grow, or capture is unsupported here): these rounds run
+    // directly, under the shared lock again; the shape is captured anew when it comes back,
+    // and after two abandoned captures the engine launches directly from then on
+    if (++h->graph_failures >= 2) h->use_graphs = false;
+    return run_rounds();
   }
   HIPCHK(hipGraphLaunch(h->rg.exec, h->stream));
   account();
