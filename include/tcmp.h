@@ -347,6 +347,22 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
                       int64_t cap_rows, int64_t* out_ids, int64_t* out_rows, double* out_data,
                       int64_t* n_queries, int64_t* n_rows);
 
+/* The two host-side halves of tcmp_gather_paths around its transport (RCCL send/recv on the
+ * GPU; any byte transport works the same way).
+ * tcmp_gather_pack: one rank's wire form -- hdr (2 n_local int64: id, rows of each path) and
+ * body (sum(rows) x 22 doubles, the paths' rows concatenated; body may alias data).
+ * tcmp_gather_unpack (rank 0): hdr_all / body_all hold every rank's wire form at the offsets of
+ * tcmp_gather_layout(world, sizes); each rank's header rows are checked against the rows it
+ * announced in sizes (status -6 otherwise: a transport that lost, duplicated or misplaced part
+ * of a message), then the outputs are written as tcmp_gather_paths writes them (status -4
+ * when the capacities are too small, n_queries / n_rows set).  Host only, no GPU. */
+int tcmp_gather_pack(int32_t n_local, const int64_t* ids, const int64_t* rows, const double* data,
+                     int64_t* hdr, double* body);
+int tcmp_gather_unpack(int32_t world, const int64_t* sizes, const int64_t* hdr_all,
+                       const double* body_all, int64_t cap_queries, int64_t cap_rows,
+                       int64_t* out_ids, int64_t* out_rows, double* out_data, int64_t* n_queries,
+                       int64_t* n_rows);
+
 /* rank 0's receive layout of tcmp_gather_paths, host only: from sizes (world x 2: queries,
  * rows per rank) each rank's first header row q_off[k] and first trajectory row r_off[k] in
  * the rank-ordered output, and the totals.  Any output pointer may be NULL. */

@@ -19,7 +19,11 @@ round -- k_edges<true,2>, the bench's own last-round kernel -- seed 1234) does n
 in three rounds (no seed of 1234..1249 does within five, tools/c5_fixture_search.py), so it pins
 the tree (status 2); the goal path at C5 scale stays pinned by the c5 fixture.
 
-    python tests/golden/gen_fullsize.py [c3] [c5] [c5b]
+C4's per-GPU shape at N = 8 (c4: eight queries bench.make_query(1234 + q), q = 0..7, 16 boxes,
+5 kg, rne, 1e5 samples each at B = 65,536, sample seed 5000 + q) -- the GPU test plans them on
+eight engines from eight host threads at once, as bench.py's C4 does.
+
+    python tests/golden/gen_fullsize.py [c3] [c5] [c5b] [c4]
 """
 import hashlib
 import os
@@ -78,6 +82,44 @@ def pack_digest(pack):
     return h.hexdigest()
 
 
+def query_record(obs, pack, goal, samples, batch, seed, n_mesh):
+    """The oracle's batched plan of one query, as the fixtures store it."""
+    O.set_meshes(pack if n_mesh else None)
+    ref = O.rrt_run(START, goal, samples, obs if len(obs) else None, 2, 5.0, 5.0, batch=batch,
+                    seed=seed, cull=2, threads=THREADS, tree=True)
+    O.set_meshes(None)
+    K = ref["n_traj"]
+    sel = np.arange(0, K, TRAJ_STRIDE)
+    return ref, dict(obs=obs, goal=goal, samples=samples, batch=batch, seed=seed, n_mesh=n_mesh,
+                     status=ref["status"], n_nodes=ref["n_nodes"], n_samples=ref["n_samples"],
+                     edge_steps=ref["edge_steps"], goal_node=ref["goal_node"],
+                     n_waypoints=ref["n_waypoints"], n_traj=K, first_fail=ref["first_fail"],
+                     n_rewires=ref["n_rewires"], waypoints=ref["waypoints"], traj_sel=sel,
+                     q=ref["q"][sel], qd=ref["qd"][sel], qdd=ref["qdd"][sel],
+                     psg=ref["psg"][sel], sha_cfg=digest(ref["tree_cfg"]),
+                     sha_cost=digest(ref["tree_cost"]),
+                     sha_parent=digest(ref["tree_parent"].astype(np.int32)))
+
+
+def make_c4(n_q=8, samples=100_000, batch=65536):
+    """C4 at N = 8: one GPU's eight queries, stored as q<k>_<field> arrays."""
+    import bench
+    eng = OracleEngine()
+    out = {"n_queries": n_q}
+    t0 = time.time()
+    for q in range(n_q):
+        obs, pack, goal = bench.make_query(1234 + q, n_obs=16, mode=2, mass=5.0, engine=eng)
+        ref, rec = query_record(obs, None, goal, samples, batch, 5000 + q, 0)
+        for k, v in rec.items():
+            out["q%d_%s" % (q, k)] = v
+        print("c4 q%d: nodes %d, steps %d, goal %d, status %d" % (
+            q, ref["n_nodes"], ref["edge_steps"], ref["goal_node"], ref["status"]), flush=True)
+    path = os.path.join(HERE, "fullsize_c4.npz")
+    np.savez_compressed(path, **out)
+    print("c4: %.0f s on %d threads -> %s" % (time.time() - t0, THREADS, os.path.getsize(path)),
+          flush=True)
+
+
 def make(name, n_obs, n_mesh, samples, batch, seed):
     import bench
     eng = OracleEngine()
@@ -111,10 +153,12 @@ def make(name, n_obs, n_mesh, samples, batch, seed):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["c3", "c5", "c5b"]
+    which = sys.argv[1:] or ["c3", "c5", "c5b", "c4"]
     if "c3" in which:
         make("c3", 16, 0, 1_000_000, 262144, 1234)
     if "c5" in which:
         make("c5", 0, 256, 131_072, 16384, 1243)
     if "c5b" in which:
         make("c5b", 0, 256, 2 * 262144 + 38528, 262144, 1234)
+    if "c4" in which:
+        make_c4()

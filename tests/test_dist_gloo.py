@@ -8,8 +8,10 @@
   around it at world sizes 2..8, ragged;
 * the two-phase rendezvous failing on every rank together (a missing rank, another job);
 * the 2-rank shard path: round-robin deal, per-rank planning (the CPU oracle stands in for the
-  GPU engine), the wire form of tcmp_gather_paths, with gloo moving the packed buffers the
-  way RCCL's send/recv does on the GPU -- torch appears only in this test harness.
+  GPU engine), each rank's wire form from libtcmp.so's own tcmp_gather_pack, gloo moving the
+  bytes to rank 0's offsets the way RCCL's send/recv does on the GPU, and rank 0's
+  tcmp_gather_unpack -- only the byte transport is not libtcmp.so's; torch appears only in
+  this test harness.
 """
 import os
 import socket
@@ -95,9 +97,9 @@ def _plan(O, qid):
 
 def _shard_worker(rank, world, port, n_queries, q):
     """One rank of the shard path: round-robin deal, planning (the oracle stands in for the
-    engine), shard.pack_paths, the size all-gather, and rank 0's staging of every rank's
-    contribution at tcmp_gather_layout's offsets (dist_helpers.stage_rank0).  gloo only carries the
-    packed buffers between the processes -- RCCL's ncclSend/ncclRecv on the GPU."""
+    engine), the rank's wire form (tcmp_gather_pack), the size all-gather, gloo carrying the
+    wire bytes to rank 0's offsets of tcmp_gather_layout (RCCL's ncclSend/ncclRecv on the
+    GPU), and rank 0's tcmp_gather_unpack."""
     sys.path.insert(0, REPO)
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import torch
@@ -105,31 +107,30 @@ def _shard_worker(rank, world, port, n_queries, q):
     sys.path.insert(0, os.path.join(REPO, "tests"))
     import dist_helpers
     import oracle as O
-    from torque_constrained_motion_planning_amd import shard
+    from torque_constrained_motion_planning_amd import _lib, shard
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ids_local = shard.queries_for_rank(n_queries, world, rank)
-    ids, rows, data = shard.pack_paths([shard.pack_trajectory(_plan(O, i)) for i in ids_local],
-                                       ids_local)
+    hdr, body = _lib.gather_pack(*shard.pack_paths(
+        [shard.pack_trajectory(_plan(O, i)) for i in ids_local], ids_local))
     sizes = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
-    dist.all_gather(sizes, torch.tensor([len(ids), int(rows.sum())], dtype=torch.int64))
+    dist.all_gather(sizes, torch.tensor([len(hdr), len(body)], dtype=torch.int64))
     sizes = torch.stack(sizes).numpy()
     if rank == 0:
-        packed = [(ids, rows, data)]
+        wires = [(hdr, body)]
         for r in range(1, world):
             nq, nr = (int(x) for x in sizes[r])
             h = torch.zeros(2 * nq, dtype=torch.int64)
             b = torch.zeros(22 * nr, dtype=torch.float64)
             dist.recv(h, src=r)
             dist.recv(b, src=r)
-            hh = h.numpy().reshape(-1, 2)
-            packed.append((hh[:, 0], hh[:, 1], b.numpy().reshape(-1, 22)))
-        got = shard.unpack_paths(*dist_helpers.stage_rank0(packed, sizes))
+            wires.append((h.numpy().reshape(-1, 2), b.numpy().reshape(-1, 22)))
+        got = shard.unpack_paths(*_lib.gather_unpack(sizes, *dist_helpers.stage_rank0(wires, sizes)))
         q.put((got, shard.gather_ok(got, range(n_queries), sizes)))
     else:
-        dist.send(torch.from_numpy(np.stack([ids, rows], 1).reshape(-1).copy()), dst=0)
-        dist.send(torch.from_numpy(data.reshape(-1).copy()), dst=0)
+        dist.send(torch.from_numpy(hdr.reshape(-1).copy()), dst=0)
+        dist.send(torch.from_numpy(body.reshape(-1).copy()), dst=0)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -145,17 +146,18 @@ def test_gather_layout_and_staging(world):
     n_q = 64
     paths = {qid: rng.normal(size=(int(rng.integers(0, 40)) * (qid % 5 != 0), 22))
              for qid in range(n_q)}
-    packed = []
+    wires = []
     for r in range(world):
         mine = shard.queries_for_rank(n_q, world, r) if r != 1 else []  # rank 1 plans nothing
-        packed.append(shard.pack_paths([paths[i] for i in mine], mine))
-    sizes = np.array([[len(i), int(rw.sum())] for i, rw, _ in packed], dtype=np.int64)
+        wires.append(_lib.gather_pack(*shard.pack_paths([paths[i] for i in mine], mine)))
+    sizes = np.array([[len(h), len(b)] for h, b in wires], dtype=np.int64)
     q_off, r_off, tq, tr = _lib.gather_layout(sizes)
     assert tq == sizes[:, 0].sum() and tr == sizes[:, 1].sum()
     assert q_off[0] == 0 and r_off[0] == 0
     assert np.array_equal(np.diff(q_off), sizes[:-1, 0]) and np.array_equal(np.diff(r_off), sizes[:-1, 1])
-    ids, rows, body = dist_helpers.stage_rank0(packed, sizes)
-    assert (ids >= 0).all() and not np.isnan(body).any()  # every slot written exactly
+    hdr, staged = dist_helpers.stage_rank0(wires, sizes)
+    assert (hdr >= 0).all() and not np.isnan(staged).any()  # every slot written exactly
+    ids, rows, body = _lib.gather_unpack(sizes, hdr, staged)
     got = shard.unpack_paths(ids, rows, body)
     expect = [i for r in range(world) if r != 1 for i in shard.queries_for_rank(n_q, world, r)]
     assert shard.gather_ok(got, expect, sizes)
@@ -167,6 +169,15 @@ def test_gather_layout_and_staging(world):
     assert not shard.gather_ok(got, expect + [999], sizes)
     with pytest.raises(_lib.TcmpError):
         _lib.gather_layout(-sizes - 1)
+    # a header row lost or misplaced in transit: rank 0's unpacking refuses it (status -6)
+    bad = hdr.copy()
+    k = int(np.argmax(bad[:, 1]))
+    bad[k, 1] += 1
+    with pytest.raises(_lib.TcmpError, match="announced"):
+        _lib.gather_unpack(sizes, bad, staged)
+    # too small an output: the capacity error of tcmp_gather_paths
+    with pytest.raises(_lib.TcmpError, match="capacity"):
+        _lib.gather_unpack(sizes, hdr, staged, cap_rows=max(0, tr - 1))
 
 
 def _rdzv_fail_worker(rank, world, port, job, q):

@@ -185,3 +185,60 @@ def test_bench_query_vs_oracle_fixture(eng, name):
         for k in ("q", "qd", "qdd"):
             assert np.abs(out[k][sel] - F[k]).max() < 1e-9, k
         assert np.abs(out["psg"][sel] - F["psg"]).max() < 1e-12
+
+
+def test_c4_eight_concurrent_queries_vs_oracle_fixture():
+    """C4's per-GPU shape at N = 8 (BASELINE configs[3]): eight 16-box rne queries of 1e5 samples
+    at B = 65,536 planned at once on eight engines from eight host threads (bench.py's C4 path),
+    each bit for bit against the oracle's batched restatement (tests/golden/fullsize_c4.npz:
+    bench.make_query(1234 + q), sample seed 5000 + q) -- tree digests, counters, waypoints and
+    trajectory rows."""
+    import os
+    import sys
+    import threading
+    from torque_constrained_motion_planning_amd import _lib
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_c4.npz")
+    if not os.path.exists(path):
+        pytest.skip("fixture not generated")
+    F = np.load(path)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    n_q = int(F["n_queries"])
+    engines = [_lib.Engine(0) for _ in range(n_q)]
+    queries = [bench.make_query(1234 + q, n_obs=16, mode=2, mass=5.0, engine=engines[q])
+               for q in range(n_q)]
+    for q, (obs, pack, goal) in enumerate(queries):
+        assert np.array_equal(obs, F["q%d_obs" % q]) and np.array_equal(goal, F["q%d_goal" % q])
+    got = [None] * n_q
+    go = threading.Barrier(n_q)
+
+    def lane(q):
+        go.wait()
+        obs, pack, goal = queries[q]
+        r, out = bench.run_query(engines[q], obs, goal, int(F["q%d_samples" % q]),
+                                 int(F["q%d_batch" % q]), int(F["q%d_seed" % q]))
+        cfg, cost, par, n = engines[q].plan_tree(r.n_nodes)
+        got[q] = (r, out, cfg, cost, par)
+
+    ts = [threading.Thread(target=lane, args=(q,)) for q in range(n_q)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    for q in range(n_q):
+        f = lambda k: F["q%d_%s" % (q, k)]  # noqa: E731
+        r, out, cfg, cost, par = got[q]
+        assert (r.n_samples, r.n_nodes, r.edge_steps, r.goal_node, r.status) == \
+            (int(f("n_samples")), int(f("n_nodes")), int(f("edge_steps")), int(f("goal_node")),
+             int(f("status"))), q
+        assert _digest(cfg) == str(f("sha_cfg")) and _digest(cost) == str(f("sha_cost"))
+        assert _digest(par.astype(np.int32)) == str(f("sha_parent"))
+        if int(f("status")) in (0, 3):
+            assert (r.n_waypoints, r.n_traj) == (int(f("n_waypoints")), int(f("n_traj")))
+            assert np.array_equal(out["waypoints"], f("waypoints"))
+            sel = f("traj_sel")
+            for k in ("q", "qd", "qdd"):
+                assert np.abs(out[k][sel] - f(k)).max() < 1e-9, (q, k)
+    assert sum(int(F["q%d_status" % q]) == 0 for q in range(n_q)) >= 2  # solved paths among them
+    for e in engines:
+        e.close()

@@ -34,7 +34,7 @@ EXPORTS = [
     "tcmp_debug_counters", "tcmp_microbench",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
     "tcmp_dist_barrier", "tcmp_dist_allreduce", "tcmp_dist_allgather_i64", "tcmp_gather_paths",
-    "tcmp_gather_layout", "tcmp_dist_rccl_ranks",
+    "tcmp_gather_layout", "tcmp_gather_pack", "tcmp_gather_unpack", "tcmp_dist_rccl_ranks",
 ]
 TRAJ_COLS = 22
 REDUCE_SUM, REDUCE_MAX = 0, 1
@@ -154,6 +154,10 @@ def load_library(path=LIB_PATH):
         L.tcmp_gather_paths.argtypes = [vp, i32, _i64p, _i64p, _dp, _i64p, ctypes.c_int64,
                                         ctypes.c_int64, _i64p, _i64p, _dp, _i64p, _i64p]
         L.tcmp_gather_layout.argtypes = [i32, _i64p, _i64p, _i64p, _i64p, _i64p]
+        if hasattr(L, "tcmp_gather_pack"):  # absent from A/B builds of older sources
+            L.tcmp_gather_pack.argtypes = [i32, _i64p, _i64p, _dp, _i64p, _dp]
+            L.tcmp_gather_unpack.argtypes = [i32, _i64p, _i64p, _dp, ctypes.c_int64,
+                                             ctypes.c_int64, _i64p, _i64p, _dp, _i64p, _i64p]
         L.tcmp_dist_rccl_ranks.argtypes = [vp, _i32p]
         _lib = L
         return L
@@ -558,6 +562,39 @@ def gather_layout(sizes):
                                             ro.ctypes.data_as(_i64p), ctypes.byref(tq),
                                             ctypes.byref(tr)))
     return qo, ro, tq.value, tr.value
+
+
+def gather_pack(ids, rows, data):
+    """tcmp_gather_pack: one rank's wire form of tcmp_gather_paths -- (hdr (n, 2) int64 of
+    (id, rows), body (sum(rows), 22) float64), the bytes its transport sends to rank 0."""
+    ids = np.ascontiguousarray(ids, dtype=np.int64)
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    data = np.ascontiguousarray(data, dtype=np.float64).reshape(-1, TRAJ_COLS)
+    hdr = np.zeros((len(ids), 2), dtype=np.int64)
+    body = np.zeros((max(int(rows.sum()) if len(rows) else 0, 0), TRAJ_COLS))
+    check(load_library().tcmp_gather_pack(len(ids), ids.ctypes.data_as(_i64p),
+                                          rows.ctypes.data_as(_i64p), _d(data),
+                                          hdr.ctypes.data_as(_i64p), _d(body)))
+    return hdr, body
+
+
+def gather_unpack(sizes, hdr_all, body_all, cap_queries=None, cap_rows=None):
+    """tcmp_gather_unpack (rank 0): every rank's wire form staged at tcmp_gather_layout's
+    offsets -> (ids, rows, data) as tcmp_gather_paths returns them."""
+    sz = np.ascontiguousarray(np.asarray(sizes, dtype=np.int64).reshape(-1, 2))
+    hdr_all = np.ascontiguousarray(hdr_all, dtype=np.int64).reshape(-1, 2)
+    body_all = np.ascontiguousarray(body_all, dtype=np.float64).reshape(-1, TRAJ_COLS)
+    cq = len(hdr_all) if cap_queries is None else int(cap_queries)
+    cr = len(body_all) if cap_rows is None else int(cap_rows)
+    oi = np.zeros(max(cq, 1), dtype=np.int64)
+    orows = np.zeros(max(cq, 1), dtype=np.int64)
+    od = np.zeros((max(cr, 1), TRAJ_COLS))
+    nq, nr = ctypes.c_int64(0), ctypes.c_int64(0)
+    check(load_library().tcmp_gather_unpack(len(sz), sz.ctypes.data_as(_i64p),
+                                            hdr_all.ctypes.data_as(_i64p), _d(body_all), cq, cr,
+                                            oi.ctypes.data_as(_i64p), orows.ctypes.data_as(_i64p),
+                                            _d(od), ctypes.byref(nq), ctypes.byref(nr)))
+    return oi[:nq.value], orows[:nq.value], od[:nr.value]
 
 
 def rendezvous(rank, world, addr, port, blob, timeout_ms=60000):

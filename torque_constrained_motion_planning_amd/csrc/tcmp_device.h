@@ -1070,10 +1070,13 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 // (4) (inner box subset hull subset outer OBB), so the answer is exactly (4)'s.
 // ------------------------------------------------------------------------------------------
 // wave totals (wave-uniform: popcounts of ballots, so they stay in SGPRs)
+// Wave totals (wave-uniform, SGPRs).  Tier-0 tests are counted as live lane-steps: the wave
+// total of 10 x n_obs tests per live lane overflowed 32 bits after ~26k steps of one
+// persistent wave at 256 meshes; pairs_tested() scales them in 64 bits.
 struct StepStats {
-  unsigned pairs_tested;  // tier-1 tests
-  unsigned pairs_sat;     // tier-2/3 evaluations
-  unsigned pairs_exact;   // tier-4 evaluations
+  unsigned live_steps;    // lane-steps that tested their obstacle pairs (tier 0)
+  unsigned pairs_sat;     // tier-2/3 evaluations (at most 64 per flush pass)
+  unsigned pairs_exact;   // tier-4 evaluations (one per wave-serial exact test)
 #ifdef TCMP_PROF
   unsigned long long cyc_exact = 0;  // shader clocks spent in tier 4 (profiling builds)
   unsigned long long cyc_t123 = 0;   // ... in tiers 1-3 (maybe branch, excluding tier 4)
@@ -1542,7 +1545,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #endif
   };
   // ---- phase A ------------------------------------------------------------------------
-  st.pairs_tested += 10u * (unsigned)sc.n_obs * (unsigned)__popcll(__ballot(live));
+  st.live_steps += (unsigned)__popcll(__ballot(live));
   // A queue that fills up is flushed after the loop and phase A resumes at (o_res, l_res);
   // the link AABBs are rebuilt on resume, so nothing of phase A is live across a flush.
   int o_res = 0, l_res = 0;

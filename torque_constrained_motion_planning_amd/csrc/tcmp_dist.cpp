@@ -355,6 +355,59 @@ int tcmp_gather_layout(int32_t world, const int64_t* sizes, int64_t* q_off, int6
   return 0;
 }
 
+int tcmp_gather_pack(int32_t n_local, const int64_t* ids, const int64_t* rows, const double* data,
+                     int64_t* hdr, double* body) {
+  if (n_local < 0 || (n_local > 0 && (!ids || !rows || !hdr))) return fail(-1, "bad arguments");
+  int64_t my_rows = 0;
+  for (int i = 0; i < n_local; ++i) {
+    if (rows[i] < 0) return fail(-1, "negative row count");
+    my_rows += rows[i];
+  }
+  if (my_rows > 0 && (!data || !body)) return fail(-1, "null trajectory rows");
+  for (int i = 0; i < n_local; ++i) {
+    hdr[2 * i] = ids[i];
+    hdr[2 * i + 1] = rows[i];
+  }
+  if (my_rows && body != data) std::memmove(body, data, (size_t)my_rows * kCols * sizeof(double));
+  return 0;
+}
+
+int tcmp_gather_unpack(int32_t world, const int64_t* sizes, const int64_t* hdr_all,
+                       const double* body_all, int64_t cap_queries, int64_t cap_rows,
+                       int64_t* out_ids, int64_t* out_rows, double* out_data, int64_t* n_queries,
+                       int64_t* n_rows) {
+  if (world < 1 || !sizes || !n_queries || !n_rows) return fail(-1, "bad arguments");
+  std::vector<int64_t> q_off((size_t)world), r_off((size_t)world);
+  int64_t tq = 0, tr = 0;
+  if (int rc = tcmp_gather_layout(world, sizes, q_off.data(), r_off.data(), &tq, &tr)) return rc;
+  *n_queries = tq;
+  *n_rows = tr;
+  if ((tq && !hdr_all) || (tr && !body_all)) return fail(-1, "null staged wire form");
+  // every rank's header rows must add up to the rows it announced: a transport that dropped,
+  // duplicated or misplaced part of a rank's message fails here, not in the caller's unpacking
+  for (int k = 0; k < world; ++k) {
+    int64_t s = 0;
+    for (int64_t i = 0; i < sizes[2 * k]; ++i) {
+      const int64_t r = hdr_all[2 * (q_off[k] + i) + 1];
+      if (r < 0) return fail(-6, "rank " + std::to_string(k) + ": negative row count received");
+      s += r;
+    }
+    if (s != sizes[2 * k + 1])
+      return fail(-6, "rank " + std::to_string(k) + ": header rows " + std::to_string(s) +
+                          " against " + std::to_string(sizes[2 * k + 1]) + " announced");
+  }
+  if (tq > cap_queries || tr > cap_rows)
+    return fail(-4, "gather output capacity too small (need " + std::to_string(tq) + " queries, " +
+                        std::to_string(tr) + " rows)");
+  if ((tq && (!out_ids || !out_rows)) || (tr && !out_data)) return fail(-1, "null output arrays");
+  for (int64_t i = 0; i < tq; ++i) {
+    out_ids[i] = hdr_all[2 * i];
+    out_rows[i] = hdr_all[2 * i + 1];
+  }
+  if (tr) std::memcpy(out_data, body_all, (size_t)tr * kCols * sizeof(double));
+  return 0;
+}
+
 int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const int64_t* rows,
                       const double* data, const int64_t* sizes_in, int64_t cap_queries,
                       int64_t cap_rows, int64_t* out_ids, int64_t* out_rows, double* out_data,
@@ -384,11 +437,10 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
   tcmp_dist::gather_layout(W, sizes.data(), q_off.data(), r_off.data(), &tq, &tr);
   *n_queries = c->rank == 0 ? tq : 0;
   *n_rows = c->rank == 0 ? tr : 0;
+  // this rank's wire form (tcmp_gather_pack: the body is the caller's rows as they lie)
   std::vector<int64_t> hdr(2 * (size_t)n_local);
-  for (int i = 0; i < n_local; ++i) {
-    hdr[2 * i] = ids[i];
-    hdr[2 * i + 1] = rows[i];
-  }
+  if (int rc = tcmp_gather_pack(n_local, ids, rows, data, hdr.data(), const_cast<double*>(data)))
+    return rc;
   std::vector<int64_t> all_hdr;
   std::vector<double> all_body;
   if (W > 1) {
@@ -441,16 +493,9 @@ int tcmp_gather_paths(tcmp_comm* c, int32_t n_local, const int64_t* ids, const i
     all_body.assign(data, data + (size_t)my_rows * kCols);
   }
   if (c->rank != 0) return 0;
-  if (tq > cap_queries || tr > cap_rows)
-    return fail(-4, "gather output capacity too small (need " + std::to_string(tq) + " queries, " +
-                        std::to_string(tr) + " rows)");
-  if ((tq && (!out_ids || !out_rows)) || (tr && !out_data)) return fail(-1, "null output arrays");
-  for (int64_t i = 0; i < tq; ++i) {
-    out_ids[i] = all_hdr[2 * i];
-    out_rows[i] = all_hdr[2 * i + 1];
-  }
-  if (tr) std::memcpy(out_data, all_body.data(), all_body.size() * sizeof(double));
-  return 0;
+  // rank 0: every rank's wire form at tcmp_gather_layout's offsets -> the outputs
+  return tcmp_gather_unpack(W, sizes.data(), all_hdr.data(), all_body.data(), cap_queries,
+                            cap_rows, out_ids, out_rows, out_data, n_queries, n_rows);
 }
 
 int tcmp_dist_rccl_ranks(const tcmp_comm* c, int32_t* n) {

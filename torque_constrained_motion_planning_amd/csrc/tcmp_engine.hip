@@ -577,7 +577,8 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
   // steps: a wave total for SPLIT == 1, per group leader otherwise; ss: wave totals
   const unsigned long long a = SPLIT == 1 ? (unsigned long long)steps
                                           : wave_sum_u64((unsigned long long)steps),
-                           b = ss.pairs_tested, c = ss.pairs_sat, d = ss.pairs_exact;
+                           b = 10ull * (unsigned long long)sc_g.n_obs * ss.live_steps,
+                           c = ss.pairs_sat, d = ss.pairs_exact;
   if (lane == 0) {
     atomicAdd(&st->edge_steps, a);
     atomicAdd(&st->pairs_tested, b);
@@ -782,10 +783,21 @@ __global__ __launch_bounds__(256) void k_mb_fp32(double* out, int iters) {
   for (int k = 0; k < kMbAcc; ++k) s += acc[k].x + acc[k].y;
   if (s == 12345.678f) out[0] = s;
 }
+// one pass, no grid stride: each thread moves kMbCopyV float4 (all loads in flight before the
+// stores, consecutive lanes on consecutive 16 B: 1 KiB per wave-instruction), the stores
+// nontemporal (streamed past the caches); n a multiple of 256 * kMbCopyV
+constexpr int kMbCopyV = 4;
 __global__ __launch_bounds__(256) void k_mb_copy(const float4* __restrict__ src, float4* __restrict__ dst,
                                                  long long n) {
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256)
-    dst[i] = src[i];
+  typedef float f32x4 __attribute__((ext_vector_type(4)));
+  const f32x4* s = reinterpret_cast<const f32x4*>(src);
+  f32x4* d = reinterpret_cast<f32x4*>(dst);
+  const long long base = (long long)blockIdx.x * (256 * kMbCopyV) + threadIdx.x;
+  f32x4 v[kMbCopyV];
+#pragma unroll
+  for (int k = 0; k < kMbCopyV; ++k) v[k] = s[base + 256 * k];
+#pragma unroll
+  for (int k = 0; k < kMbCopyV; ++k) __builtin_nontemporal_store(v[k], &d[base + 256 * k]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3400,7 +3412,7 @@ int tcmp_microbench(tcmp_handle* h, double* out) {
   }
   (void)hipMemsetAsync(src, 0, n4 * 16, h->stream);
   ms = best_ms([&] {
-    hipLaunchKernelGGL(k_mb_copy, dim3(std::max(1, h->cu_count) * 32), dim3(256), 0, h->stream,
+    hipLaunchKernelGGL(k_mb_copy, dim3((unsigned)(n4 / (256 * kMbCopyV))), dim3(256), 0, h->stream,
                        src, dst, (long long)n4);
   });
   out[2] = 2.0 * (double)n4 * 16 / (ms * 1e-3) / 1e9;
