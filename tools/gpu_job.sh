@@ -8,6 +8,8 @@
 #   pmc[=W]          PMC passes FETCH_SIZE / WRITE_SIZE (one run each) over one bench step
 #   sq[=W]           PMC pass of SQ wave / busy counters over one bench step
 #   valu[=W]         PMC pass of the SQ_INSTS_VALU_* / FLOPS counters over one bench step
+#   mix[=W]          PMC pass of the instruction mix (SQ_INSTS total / VALU / SALU / branch /
+#                    LDS / VMEM / SMEM, SQ_THREAD_CYCLES_VALU) over one bench step
 #   prof             profiling-build (make prof) clock breakdowns: tools/nn_profile.py and
 #                    tools/edge_profile.py on C3
 #   ab=LIBS          same-box A/B of libtcmp builds (space-separated .so paths): C3 bench lines,
@@ -64,6 +66,12 @@ for st in "$@"; do
         --kernel-trace -d $O/valu_$w -o run --output-format csv \
         -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
         --pipeline 1 --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
+    mix)
+      w=${arg:-c3}
+      timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_THREAD_CYCLES_VALU \
+        --kernel-trace -d $O/mix_$w -o run --output-format csv \
+        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
+        --pipeline 1 --no-cpu-baseline --no-alt > $O/mix_$w.log 2>&1 ;;
     prof)
       P=torque_constrained_motion_planning_amd/libtcmp_prof.so
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err

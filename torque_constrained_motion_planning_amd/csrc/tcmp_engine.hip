@@ -417,7 +417,31 @@ struct EdgeJob {
   double* last;             // stride 8
   const int* order;         // nullable: the k-th edge taken is order[k] (longest first)
   int* accepted;            // nullable: accepted edges (nsafe > 0) per 256 edges, cleared before
+  double* rec;              // the k-th edge taken, as k_edges fetches it (k_edge_records): its
+                            // from-configuration q0..q6 and (edge index, planned steps) packed
+                            // in the 8th double -- one 64-B load per fetch
 };
+
+// The work records k_edges' lanes fetch (launch_edges runs this first): record k = the edge
+// taken k-th (order[k], or k), its from-configuration (from_base[from_idx[e]] or from_base[e])
+// and its planned step count num_steps(from, to[e]) (utils.py:3072).  A fetch is then one
+// dependent load after the work counter, where it was three (order, from_idx, the rows) and a
+// num_steps on the wave-step that fetched.
+__global__ __launch_bounds__(256) void k_edge_records(EdgeJob J, const PlanParams* __restrict__ Pd) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= J.n) return;
+  const int e = J.order ? J.order[k] : k;
+  const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
+  double a[7], b[7], res[7];
+  load7(J.from_base + 8 * src, a);
+  load7(J.to + 8 * (size_t)e, b);
+#pragma unroll
+  for (int j = 0; j < 7; ++j) res[j] = Pd->res[j];
+  const int n = num_steps(a, b, res);
+  double* r = J.rec + 8 * (size_t)k;
+  *reinterpret_cast<double4*>(r) = make_double4(a[0], a[1], a[2], a[3]);
+  *reinterpret_cast<double4*>(r + 4) = make_double4(a[4], a[5], a[6], __hiloint2double(n, e));
+}
 
 #ifndef TCMP_EDGE_SPLIT
 #define TCMP_EDGE_SPLIT 4  // small rounds: up to this many lanes per edge (k_edges SPLIT)
@@ -468,14 +492,13 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
         // (the other lanes of a group take its first lane's slot: all hold the same edge)
         const int my = base + (int)__popcll(m & ((1ull << (lane - sub)) - 1ull));
         if (my < J.n) {
-          e = J.order ? J.order[my] : my;
-          const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
-          double q2[7], res[7];  // (re-read per edge: nothing of it stays live in the loop)
-#pragma unroll
-          for (int k = 0; k < 7; ++k) res[k] = Pd->res[k];
-          load7(J.from_base + 8 * src, q);
-          load7(J.to + 8 * (size_t)e, q2);
-          n = num_steps(q, q2, res);
+          // the edge's record (k_edge_records): from-configuration, edge index, planned steps
+          const double4 ra = *reinterpret_cast<const double4*>(J.rec + 8 * (size_t)my);
+          const double4 rb = *reinterpret_cast<const double4*>(J.rec + 8 * (size_t)my + 4);
+          q[0] = ra.x; q[1] = ra.y; q[2] = ra.z; q[3] = ra.w;
+          q[4] = rb.x; q[5] = rb.y; q[6] = rb.z;
+          e = __double2loint(rb.w);
+          n = __double2hiint(rb.w);
           i = 0;
         } else {
           done = true;
@@ -783,10 +806,11 @@ __global__ __launch_bounds__(256) void k_mb_fp32(double* out, int iters) {
   for (int k = 0; k < kMbAcc; ++k) s += acc[k].x + acc[k].y;
   if (s == 12345.678f) out[0] = s;
 }
-// one pass, no grid stride: each thread moves kMbCopyV float4 (all loads in flight before the
-// stores, consecutive lanes on consecutive 16 B: 1 KiB per wave-instruction), the stores
-// nontemporal (streamed past the caches); n a multiple of 256 * kMbCopyV
-constexpr int kMbCopyV = 4;
+// one pass, no grid stride: each thread moves V float4 (all loads in flight before the stores,
+// consecutive lanes on consecutive 16 B: 1 KiB per wave-instruction), the stores nontemporal
+// (streamed past the caches); n a multiple of 256 * V.  tcmp_microbench reports the best of
+// V = 2, 4, 8.
+template <int kMbCopyV>
 __global__ __launch_bounds__(256) void k_mb_copy(const float4* __restrict__ src, float4* __restrict__ dst,
                                                  long long n) {
   typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -1205,6 +1229,7 @@ struct tcmp_handle {
   DBuf<int> parent;
   DBuf<int2> meta;
   DBuf<double> cand, last;
+  DBuf<double> erec;  // k_edges' work records (k_edge_records), one per edge of a round
   DBuf<unsigned char> cgoal;
   DBuf<int> nn, nsafe, nsteps, nbr, ncount, rwlist;
   DBuf<double> nnscore;  // the last round's best exact score per candidate (tcmp_plan_debug_round)
@@ -1657,6 +1682,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool re
     split *= 2;
   if (split > 1) blocks = std::min(cap, ((long long)split * J.n + 255) / 256);
   h->edge_blocks = (int)blocks;
+  hipLaunchKernelGGL(k_edge_records, dim3(grid_for(J.n, 256)), dim3(256), 0, h->stream, J, dP);
   const bool mk = h->mesh_kernels();
   auto kern = split == 4 ? (mk ? k_edges<true, 4> : k_edges<false, 4>)
               : split == 2 ? (mk ? k_edges<true, 2> : k_edges<false, 2>)
@@ -1848,7 +1874,7 @@ int tcmp_destroy(tcmp_handle* h) {
     h->lodei[i].release();
   }
   for (auto* b : {&h->verts, &h->planes, &h->edges, &h->obs, &h->cfg, &h->tgt, &h->cand,
-                  &h->last, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
+                  &h->last, &h->erec, &h->wp, &h->tq, &h->tqd, &h->tqdd, &h->tpsg, &h->ttau, &h->s0,
                   &h->s1, &h->s2, &h->s3})
     b->release();
   for (auto* b : {&h->parent, &h->nn, &h->nsafe, &h->nsteps, &h->nbr, &h->ncount, &h->i0,
@@ -2490,7 +2516,9 @@ int tcmp_check_edges(tcmp_handle* h, const double* from, const double* to, int64
     for (int k = 0; k < 7; ++k) P.res[k] = resolutions[k];
   P.torque_mode = torque_mode;
   P.mass = payload_mass;
-  EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p, nullptr};
+  if ((rc = h->erec.ensure((size_t)n * 8))) return rc;
+  EdgeJob J{h->s0.p, nullptr, h->s1.p, (int)n, h->i0.p, h->i1.p, h->s2.p, nullptr, nullptr,
+            h->erec.p};
   HIPCHK(hipMemcpyAsync(h->dPx, &P, sizeof(P), hipMemcpyHostToDevice, h->stream));
   if ((rc = launch_edges(h, J, h->dPx))) return rc;
   std::vector<double> tmp((size_t)n * 8);
@@ -2650,6 +2678,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   rc = rc ? rc : h->chain.ensure(N);
   rc = rc ? rc : h->cand.ensure(B * 8);
   rc = rc ? rc : h->last.ensure(B * 8);
+  rc = rc ? rc : h->erec.ensure(B * 8);
   rc = rc ? rc : h->cgoal.ensure(B);
   rc = rc ? rc : h->nn.ensure(B);
   rc = rc ? rc : h->nsafe.ensure(B);
@@ -2765,6 +2794,7 @@ static unsigned long long round_graph_key(const tcmp_handle* h, long long n_samp
                         (const void*)h->cs_hist.p, (const void*)h->cvals_in.p, (const void*)h->cperm.p,
                         (const void*)h->cs_hoff.p, (const void*)h->ckeys.p,
                         (const void*)h->sort_tmp.p, (const void*)h->bcount.p, (const void*)h->boff.p,
+                        (const void*)h->erec.p,
                         (const void*)h->st, (const void*)h->dP})
     mixp(p);
   const Scene sc = h->scene();
@@ -2839,7 +2869,8 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
   if (!e1) e1 = h->mark();
   h->span(F_NEAREST, e0, e1);
   h->launches_nearest++;
-  EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p, nullptr};
+  EdgeJob J{h->cfg.p, h->nn.p, h->cand.p, nb, h->nsafe.p, h->nsteps.p, h->last.p, nullptr,
+            nullptr, h->erec.p};
   if (nb >= kEdgeOrderMin) {
     // longest planned edges first (the persistent lanes then finish together): a counting
     // sort by 255 - min(n, 255) in the candidate-sort buffers, which the nearest scan is done with
@@ -3412,9 +3443,17 @@ int tcmp_microbench(tcmp_handle* h, double* out) {
   }
   (void)hipMemsetAsync(src, 0, n4 * 16, h->stream);
   ms = best_ms([&] {
-    hipLaunchKernelGGL(k_mb_copy, dim3((unsigned)(n4 / (256 * kMbCopyV))), dim3(256), 0, h->stream,
+    hipLaunchKernelGGL(k_mb_copy<4>, dim3((unsigned)(n4 / (256 * 4))), dim3(256), 0, h->stream,
                        src, dst, (long long)n4);
   });
+  ms = std::min(ms, best_ms([&] {
+    hipLaunchKernelGGL(k_mb_copy<2>, dim3((unsigned)(n4 / (256 * 2))), dim3(256), 0, h->stream,
+                       src, dst, (long long)n4);
+  }));
+  ms = std::min(ms, best_ms([&] {
+    hipLaunchKernelGGL(k_mb_copy<8>, dim3((unsigned)(n4 / (256 * 8))), dim3(256), 0, h->stream,
+                       src, dst, (long long)n4);
+  }));
   out[2] = 2.0 * (double)n4 * 16 / (ms * 1e-3) / 1e9;
   out[3] = 0.0;
   (void)hipFree(src);
