@@ -1621,16 +1621,18 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
     for (int o = o_res; o < n_tier0 && !full; ++o) {
       unsigned lm = 0;
       if (o < sc.n_obs) {
+        // the obstacle's (hi x, hi y), (hi z, -lo x), (-lo y, -lo z), kPen-shrunk (tier0_bounds)
         const float4 oa = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o);
         const float4 ob4 = *reinterpret_cast<const float4*>(sc.obs32 + 8 * o + 4);
-        const t0f2 oA = {oa.x + ob4.x, oa.y + ob4.y};
-        const t0f2 oB = {oa.z + ob4.z, ob4.x - oa.x};
-        const t0f2 oC = {ob4.y - oa.y, ob4.z - oa.z};
+        const t0f2 oA = {oa.x, oa.y};
+        const t0f2 oB = {oa.z, ob4.x};
+        const t0f2 oC = {ob4.y, ob4.z};
 #pragma unroll
         for (int l = 0; l < 10; ++l) {
           const t0f2 d1 = t0a[l] - oA, d2 = t0b[l] - oB, d3 = t0c[l] - oC;
-          const float m = fmaxf(fmaxf(fmaxf(d1.x, d1.y), fmaxf(d2.x, d2.y)), fmaxf(d3.x, d3.y));
-          lm |= (__float_as_uint(m) >> 31) << l;  // m < 0: overlap on every axis
+          // all six negative (overlap on every axis): the sign bits of two v_max3 results
+          const float mx = fmaxf(fmaxf(d1.x, d1.y), d2.x), my = fmaxf(fmaxf(d2.y, d3.x), d3.y);
+          lm |= ((__float_as_uint(mx) & __float_as_uint(my)) >> 31) << l;
         }
       } else if (MESH) {
         const int q = o - sc.n_obs;

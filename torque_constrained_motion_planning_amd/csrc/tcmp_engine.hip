@@ -2138,6 +2138,17 @@ int upload_lods(tcmp_handle* h) {
 }
 
 
+// Tier-0 record of an obstacle (fp32, 8 floats): axis i's world-AABB bounds shrunk by kPen
+// (less a rounding margin), as tier 0 compares them -- [hi_x, hi_y, hi_z, 0, -lo_x, -lo_y,
+// -lo_z, 0] with hi = c + H', lo = c - H', H' = half extent - kPen + margin, each rounded once
+// from fp64 (the margin, 1e-5 + 1e-6 (|c| + H), covers that rounding and the link side's).
+static void tier0_bounds(float* f, int i, double c, double Hs) {
+  f[i] = (float)(c + Hs);
+  f[4 + i] = (float)(Hs - c);
+  f[3] = 0.f;
+  f[7] = 0.f;
+}
+
 int upload_scene(tcmp_handle* h) {
   const int n = h->n_box + h->n_mesh;
   const int n_self = h->self_coll ? TCMP_NLINKS : 0;
@@ -2156,8 +2167,7 @@ int upload_scene(tcmp_handle* h) {
     for (int i = 0; i < 3; ++i) {
       const double H = fabs(d[3 + 3 * i]) * d[12] + fabs(d[4 + 3 * i]) * d[13] +
                        fabs(d[5 + 3 * i]) * d[14];
-      f[i] = (float)d[i];
-      f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(d[i]) + H));
+      tier0_bounds(f, i, d[i], H - kPen + 1e-5 + 1e-6 * (fabs(d[i]) + H));
     }
   }
   for (int m = 0; m < h->n_mesh; ++m) {
@@ -2174,8 +2184,7 @@ int upload_scene(tcmp_handle* h) {
     float* f = t32.data() + 8 * (h->n_box + m);
     for (int i = 0; i < 3; ++i) {
       const double c = 0.5 * (lo[i] + hi[i]), H = 0.5 * (hi[i] - lo[i]);
-      f[i] = (float)c;
-      f[4 + i] = (float)(H - kPen + 1e-5 + 1e-6 * (fabs(c) + H));
+      tier0_bounds(f, i, c, H - kPen + 1e-5 + 1e-6 * (fabs(c) + H));
     }
   }
   // self-collision: link j's outer box in its own frame, as the record of mesh n_mesh + j
