@@ -96,8 +96,10 @@ struct Scene {
   const float* __restrict__ obs32;   // [n][8]: world-AABB centre(3), H - kPen + margin (3)
   unsigned* wq;                      // this wave's LDS pair queue (collides_wave), kQcap + 2
   // convex-mesh obstacles (tcmp_set_meshes), world frame, global memory
-  const int* __restrict__ mrange;    // [m][24]: v0 v1 f0 f1 e0 e1 (rows of the arrays below),
-                                     // the same for the inner / outer LODs, has-LOD flag
+  const int* __restrict__ mrange;    // [m][32]: v0 v1 f0 f1 e0 e1 (rows of the arrays below),
+                                     // the same for the inner / outer LODs [6..17], has-LOD
+                                     // flag [18], spheres flag [19], Gauss-map clusters of the
+                                     // full hull [20, 21) and of the LODs [22..25]
   const double* __restrict__ mib;    // [m][16]: inner box record (c, B, inner half, 0)
   const double4* __restrict__ mv64;  // [V]: x y z 0
   const float4* __restrict__ mv32;
@@ -105,10 +107,12 @@ struct Scene {
   const float4* __restrict__ mp32;
   const double* __restrict__ me64;   // [E][16]: c = -n1, d = -n2, dxc = unit(d x c), e, v0
   const float* __restrict__ me32;    // [E][16]
+  const float4* __restrict__ mcl;    // Gauss-map clusters of me32's records (HullB32::cl)
   // level-of-detail hulls of the meshes ([0] inner, [1] outer; mrange [6..17], flag [18])
   const float4* lv32[2];
   const float4* lp32[2];
   const float* le32[2];
+  const float4* lcl[2];              // Gauss-map clusters of le32's records
   // the links' level-of-detail hulls (panda_lod.inc), fp32 link frames: [0] inner, [1] outer
   const float* lodv3[2];
   const float4* lodpl[2];
@@ -130,7 +134,7 @@ struct Scene {
   int n_mesh;
   int self_coll;
 };
-constexpr int kMrange = 24;  // ints per mesh in Scene::mrange
+constexpr int kMrange = 32;  // ints per mesh in Scene::mrange
 __device__ __forceinline__ int obs_mesh(const double* ob) {
   return ob[15] < 0.0 ? (int)(-ob[15]) - 1 : -1;
 }
@@ -1013,7 +1017,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
                      tcmp_lod_in_vert_off[link + 1], tcmp_lod_in_plane_off[link],
                      tcmp_lod_in_plane_off[link + 1], tcmp_lod_in_edge_off[link],
                      tcmp_lod_in_edge_off[link + 1]};
-    const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11]};
+    const HullB32 Bi{sc.lv32[0], sc.lp32[0], sc.le32[0], rg[6], rg[7], rg[8], rg[9], rg[10], rg[11],
+                     sc.lcl[0], rg[22], rg[23]};
     return hull_hull_wave32<false>(Ai, Bi, R, p, P + kExactGuard);
   };
   if (inner_first) {
@@ -1029,7 +1034,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
                      tcmp_lod_out_vert_off[link + 1], tcmp_lod_out_plane_off[link],
                      tcmp_lod_out_plane_off[link + 1], tcmp_lod_out_edge_off[link],
                      tcmp_lod_out_edge_off[link + 1]};
-    const HullB32 Bo{sc.lv32[1], sc.lp32[1], sc.le32[1], rg[12], rg[13], rg[14], rg[15], rg[16], rg[17]};
+    const HullB32 Bo{sc.lv32[1], sc.lp32[1], sc.le32[1], rg[12], rg[13], rg[14], rg[15], rg[16], rg[17],
+                     sc.lcl[1], rg[24], rg[25]};
     const float pl = hull_hull_wave32<false>(Ao, Bo, R, p, P - kExactGuard);
     TCMP_MESH_CLK(1);
     if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); return (double)pl; }
@@ -1048,7 +1054,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   const HullA32 A{g.verts32, g.planes32, g.eidx, sc.geo_ev, tcmp_geo_vert_off[link],
                   tcmp_geo_vert_off[link + 1], tcmp_geo_plane_off[link],
                   tcmp_geo_plane_off[link + 1], tcmp_geo_edge_off[link], tcmp_geo_edge_off[link + 1]};
-  const HullB32 B{sc.mv32, sc.mp32, sc.me32, rg[0], rg[1], rg[2], rg[3], rg[4], rg[5]};
+  const HullB32 B{sc.mv32, sc.mp32, sc.me32, rg[0], rg[1], rg[2], rg[3], rg[4], rg[5], sc.mcl,
+                  rg[20], rg[21]};
   const float pm = hull_hull_wave32<true>(A, B, R, p, P - kExactGuard);
   TCMP_MESH_CLK(3);
   if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;

@@ -1204,6 +1204,7 @@ struct tcmp_handle {
   DBuf<double> base_pd;
   DBuf<float> mv32, mp32, me32;
   DBuf<float> lv32[2], lp32[2], le32[2];      // mesh LOD hulls (inner, outer), world frame
+  DBuf<float> mcl, lcl[2];                    // Gauss-map clusters of me32 / le32 (gauss_clusters)
   // host copies of the user meshes' LOD hulls (tcmp_set_mesh_lods; cleared by tcmp_set_meshes)
   bool user_lods = false;
   std::vector<double> lod_v[2], lod_p[2];
@@ -1309,10 +1310,12 @@ struct tcmp_handle {
     s.mp32 = reinterpret_cast<const float4*>(mp32.p);
     s.me64 = me64.p;
     s.me32 = me32.p;
+    s.mcl = reinterpret_cast<const float4*>(mcl.p);
     for (int i = 0; i < 2; ++i) {
       s.lv32[i] = reinterpret_cast<const float4*>(lv32[i].p);
       s.lp32[i] = reinterpret_cast<const float4*>(lp32[i].p);
       s.le32[i] = le32[i].p;
+      s.lcl[i] = reinterpret_cast<const float4*>(lcl[i].p);
       s.lodv3[i] = lodv3[i].p;
       s.lodpl[i] = reinterpret_cast<const float4*>(lodpl[i].p);
       s.lodei[i] = reinterpret_cast<const ushort4*>(lodei[i].p);
@@ -1867,7 +1870,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->obs32.release();
   h->mrange.release();
   for (auto* b : {&h->mib, &h->mv64, &h->mp64, &h->me64, &h->base_geo, &h->base_pd}) b->release();
-  for (auto* b : {&h->mv32, &h->mp32, &h->me32}) b->release();
+  for (auto* b : {&h->mv32, &h->mp32, &h->me32, &h->mcl, &h->lcl[0], &h->lcl[1]}) b->release();
   for (int i = 0; i < 2; ++i) {
     for (auto* b : {&h->lv32[i], &h->lp32[i], &h->le32[i], &h->lodv3[i], &h->lodpl[i], &h->lodev[i]})
       b->release();
@@ -1948,6 +1951,89 @@ void edge_records(const double* verts, const int32_t* vert_off, const double* pl
     }
 }
 
+// Sorts the Gauss-map records [e0, e1) of one hull (rows of 16 doubles, edge_records) by the
+// direction of their arcs -- the arc c -> d lies in the cone (unit(c + d), half the c-d angle)
+// -- and cuts them into at most kMaxGaussClusters clusters of consecutive records, appending
+// each cluster's cone to cl (8 floats: axis, cos, sin of the half-angle, first and end record
+// as int bits, 0): the axis is the normalized sum of its arcs' axes, the half-angle the largest
+// (angle to an arc's axis + that arc's half-angle), plus 1e-3 rad.  Returns the clusters'
+// index range in cl through c0 / c1.  Record order does not matter anywhere else (every
+// consumer takes a minimum over all records).
+void gauss_clusters(double* rec, int e0, int e1, std::vector<float>& cl, int* c0, int* c1) {
+  const int n = e1 - e0;
+  *c0 = (int)(cl.size() / 8);
+  if (n <= 0) {
+    *c1 = *c0;
+    return;
+  }
+  struct Arc {
+    double ax[3], half;
+    unsigned key;
+    int row;
+  };
+  std::vector<Arc> arcs((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const double* r = rec + 16 * (size_t)(e0 + i);
+    Arc& a = arcs[(size_t)i];
+    double s[3] = {r[0] + r[3], r[1] + r[4], r[2] + r[5]};
+    const double sl = sqrt(s[0] * s[0] + s[1] * s[1] + s[2] * s[2]);
+    const double cd = std::max(-1.0, std::min(1.0, r[0] * r[3] + r[1] * r[4] + r[2] * r[5]));
+    if (sl > 1e-9) {
+      for (int k = 0; k < 3; ++k) a.ax[k] = s[k] / sl;
+      a.half = 0.5 * acos(cd);
+    } else {  // antipodal normals: no cone smaller than the sphere
+      a.ax[0] = 1; a.ax[1] = 0; a.ax[2] = 0;
+      a.half = 3.14159265358979323846;
+    }
+    // cube-map face of the axis, then a 4-bit-per-coordinate Morton code on that face
+    int f = 0;
+    for (int k = 1; k < 3; ++k)
+      if (fabs(a.ax[k]) > fabs(a.ax[f])) f = k;
+    const int u = (f + 1) % 3, v = (f + 2) % 3;
+    const double m = fabs(a.ax[f]) > 0 ? fabs(a.ax[f]) : 1.0;
+    const unsigned qu = (unsigned)std::min(15.0, std::max(0.0, (a.ax[u] / m + 1.0) * 8.0));
+    const unsigned qv = (unsigned)std::min(15.0, std::max(0.0, (a.ax[v] / m + 1.0) * 8.0));
+    unsigned mort = 0;
+    for (int b = 3; b >= 0; --b) mort = (mort << 2) | (((qu >> b) & 1u) << 1) | ((qv >> b) & 1u);
+    a.key = ((unsigned)(2 * f + (a.ax[f] < 0 ? 1 : 0)) << 8) | mort;
+    a.row = e0 + i;
+  }
+  std::stable_sort(arcs.begin(), arcs.end(), [](const Arc& x, const Arc& y) { return x.key < y.key; });
+  std::vector<double> tmp((size_t)n * 16);
+  for (int i = 0; i < n; ++i)
+    memcpy(tmp.data() + 16 * (size_t)i, rec + 16 * (size_t)arcs[(size_t)i].row, 16 * sizeof(double));
+  memcpy(rec + 16 * (size_t)e0, tmp.data(), tmp.size() * sizeof(double));
+  const int K = std::max(8, (n + kMaxGaussClusters - 1) / kMaxGaussClusters);
+  for (int s0 = 0; s0 < n; s0 += K) {
+    const int s1 = std::min(n, s0 + K);
+    double b[3] = {0, 0, 0};
+    for (int i = s0; i < s1; ++i)
+      for (int k = 0; k < 3; ++k) b[k] += arcs[(size_t)i].ax[k];
+    const double bl = sqrt(b[0] * b[0] + b[1] * b[1] + b[2] * b[2]);
+    double half = 0.0;
+    if (bl > 1e-9) {
+      for (int k = 0; k < 3; ++k) b[k] /= bl;
+      for (int i = s0; i < s1; ++i) {
+        const Arc& a = arcs[(size_t)i];
+        const double c = std::max(-1.0, std::min(1.0, b[0] * a.ax[0] + b[1] * a.ax[1] + b[2] * a.ax[2]));
+        half = std::max(half, acos(c) + a.half);
+      }
+      half += 1e-3;
+    } else {
+      b[0] = 1; b[1] = 0; b[2] = 0;
+      half = 3.14159265358979323846;
+    }
+    half = std::min(half, 3.14159265358979323846);
+    int r0 = e0 + s0, r1 = e0 + s1;
+    float f[8] = {(float)b[0], (float)b[1], (float)b[2], (float)cos(half), (float)sin(half), 0.f, 0.f,
+                  0.f};
+    memcpy(&f[5], &r0, 4);
+    memcpy(&f[6], &r1, 4);
+    cl.insert(cl.end(), f, f + 8);
+  }
+  *c1 = (int)(cl.size() / 8);
+}
+
 int check_hulls(const tcmp_hulls* H, int n, const char* what) {
   if (!H || !H->verts || !H->vert_off || !H->planes || !H->plane_off || !H->edges || !H->edge_off)
     return fail(-1, std::string("null ") + what + " hull array");
@@ -2015,6 +2101,11 @@ int upload_meshes(tcmp_handle* h) {
   }
   edge_records(verts.data(), vert_off.data(), planes.data(), plane_off.data(), edges.data(),
                edge_off.data(), n_mesh, e64.data());
+  std::vector<float> mcl;
+  for (int m = 0; m < n_mesh; ++m)
+    gauss_clusters(e64.data(), edge_off[m], edge_off[m + 1], mcl, &rg[kMrange * m + 20],
+                   &rg[kMrange * m + 21]);
+  if (mcl.empty()) mcl.assign(8, 0.f);
   for (int v = 0; v < V; ++v)
     for (int k = 0; k < 3; ++k) v64[4 * v + k] = verts[3 * v + k];
   for (int f = 0; f < F; ++f)
@@ -2028,7 +2119,9 @@ int upload_meshes(tcmp_handle* h) {
   rc = rc ? rc : h->mv32.ensure(v32.size());
   rc = rc ? rc : h->mp32.ensure(p32.size());
   rc = rc ? rc : h->me32.ensure(e32.size());
+  rc = rc ? rc : h->mcl.ensure(mcl.size());
   if (rc) return rc;
+  HIPCHK(hipMemcpyAsync(h->mcl.p, mcl.data(), mcl.size() * sizeof(float), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mrange.p, rg.data(), rg.size() * sizeof(int), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mib.p, ib.data(), ib.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
   HIPCHK(hipMemcpyAsync(h->mv64.p, v64.data(), v64.size() * sizeof(double), hipMemcpyHostToDevice, h->stream));
@@ -2110,13 +2203,19 @@ int upload_lods(tcmp_handle* h) {
     const int nm = n_user + n_self, V = vo[nm], F = po[nm], E = eo[nm];
     std::vector<double> e64((size_t)E * 16);
     edge_records(v.data(), vo.data(), pl.data(), po.data(), e.data(), eo.data(), nm, e64.data());
+    std::vector<float> lcl;
+    std::vector<int> cr(2 * (size_t)nm);
+    for (int m = 0; m < nm; ++m) gauss_clusters(e64.data(), eo[m], eo[m + 1], lcl, &cr[2 * m], &cr[2 * m + 1]);
+    if (lcl.empty()) lcl.assign(8, 0.f);
     std::vector<float> v32((size_t)V * 4, 0.f), p32(pl.begin(), pl.end()), e32(e64.begin(), e64.end());
     for (int r = 0; r < V; ++r)
       for (int k = 0; k < 3; ++k) v32[4 * r + k] = (float)v[3 * r + k];
     int rc = h->lv32[i].ensure(v32.size());
     rc = rc ? rc : h->lp32[i].ensure(p32.size());
     rc = rc ? rc : h->le32[i].ensure(e32.size());
+    rc = rc ? rc : h->lcl[i].ensure(lcl.size());
     if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(h->lcl[i].p, lcl.data(), lcl.size() * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->lv32[i].p, v32.data(), v32.size() * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->lp32[i].p, p32.data(), p32.size() * 4, hipMemcpyHostToDevice, h->stream));
     HIPCHK(hipMemcpyAsync(h->le32[i].p, e32.data(), e32.size() * 4, hipMemcpyHostToDevice, h->stream));
@@ -2128,6 +2227,8 @@ int upload_lods(tcmp_handle* h) {
       r[0] = vo[m]; r[1] = vo[m + 1];
       r[2] = po[m]; r[3] = po[m + 1];
       r[4] = eo[m]; r[5] = eo[m + 1];
+      rg[kMrange * mesh + 22 + 2 * i] = cr[2 * m];
+      rg[kMrange * mesh + 23 + 2 * i] = cr[2 * m + 1];
       rg[kMrange * mesh + 18] = 1;
     }
   }

@@ -39,13 +39,23 @@ struct HullA32 {
   int v0, v1, f0, f1, e0, e1;
 };
 // A world-frame obstacle hull: vertices, planes, Gauss-map edge records [E][16]
-// (c = -n1, d = -n2, unit(d x c), edge vector, endpoint).
+// (c = -n1, d = -n2, unit(d x c), edge vector, endpoint), sorted by the direction of their
+// arcs and cut into at most 32 clusters [c0, c1) of consecutive records, each with a cone on
+// the Gauss sphere holding all its arcs (gauss_clusters, tcmp_engine.hip): two float4 per
+// cluster, (axis, cos half-angle), (sin half-angle, first record, end record, 0) with the
+// record indices as int bits.
 struct HullB32 {
   const float4* v;
   const float4* pl;
   const float* er;
   int v0, v1, f0, f1, e0, e1;
+  const float4* cl;
+  int c0, c1;
 };
+constexpr int kMaxGaussClusters = 32;
+// slack on the cone test's cosine: far above the fp32 error of the rotated axes (~1e-6), so a
+// pair of arcs that intersect is never pruned
+constexpr float kConeSlack = 2e-3f;
 
 // Wave-uniform streams of read-only hull data go through the constant address space, so they
 // become scalar loads (s_load_dwordx4 / _dwordx16 into SGPRs, the scalar cache) instead of
@@ -141,15 +151,22 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
   pd = fminf(pd, wave_minf(facets32<false>(A, B, R, p)));
   if (pd < stop) { if (STAT) TCMP_MSTAT(9); return pd; }
   float loc = INFINITY;
-  // (3) edge pairs: lanes own A's edges, B's edges stream wave-uniformly
+  // (3) edge pairs whose Gauss-map arcs intersect (Gregorius' Minkowski-face test).  Lanes own
+  // A's edges, 64 at a time.  Pass 1: each lane's arc a -> b (A's facet normals in the world) is
+  // held by the cone (unit(a + b), half the a-b angle); a cluster of B's arcs can hold an arc that
+  // intersects it only if the two cones overlap, angle(axes) <= sum of half-angles -- one bit per
+  // cluster.  Pass 2: the (edge, cluster) candidates in rank order, one per lane (a wave prefix
+  // sum of the per-lane counts and a six-step binary search over the lanes, as exact_pd_wave32's
+  // edge pass): the lane rebuilds the edge and walks the cluster's records.  The axes evaluated
+  // are the unpruned loop's (the cones are conservative by kConeSlack), so the minimum is too.
   bool deg = false;
+  const int nC = B.c1 - B.c0;
   for (int base = A.e0; base < A.e1; base += 64) {
-    const int e = base + lane;
-    const bool valid = e < A.e1;
-    float ax = 0, ay = 0, az = 0, bx = 0, by = 0, bz = 0;  // adjacent facet normals (world)
-    float ux = 0, uy = 0, uz = 0;                          // unit(b x a)
-    float ex = 0, ey = 0, ez = 0, px = 0, py = 0, pz = 0;  // edge vector, endpoint (world)
-    if (valid) {
+    // this lane's edge of A in the world: adjacent facet normals a, b, unit(b x a), edge
+    // vector, endpoint
+    auto a_edge = [&](int e, float& ax, float& ay, float& az, float& bx, float& by, float& bz,
+                      float& ux, float& uy, float& uz, float& ex, float& ey, float& ez,
+                      float& px, float& py, float& pz) {
       const ushort4 ix = A.ei[e];
       const float4 na = A.pl[ix.z], nb = A.pl[ix.w];
       ax = R[0] * na.x + R[1] * na.y + R[2] * na.z;
@@ -165,47 +182,102 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
       ux *= il; uy *= il; uz *= il;
       const float x0 = A.v3[3 * ix.x], y0 = A.v3[3 * ix.x + 1], z0 = A.v3[3 * ix.x + 2];
       const float4 ed = A.ev[e];
-      const float lx = ed.x, ly = ed.y, lz = ed.z;
-      ex = R[0] * lx + R[1] * ly + R[2] * lz;
-      ey = R[3] * lx + R[4] * ly + R[5] * lz;
-      ez = R[6] * lx + R[7] * ly + R[8] * lz;
+      ex = R[0] * ed.x + R[1] * ed.y + R[2] * ed.z;
+      ey = R[3] * ed.x + R[4] * ed.y + R[5] * ed.z;
+      ez = R[6] * ed.x + R[7] * ed.y + R[8] * ed.z;
       px = R[0] * x0 + R[1] * y0 + R[2] * z0 + p[0];
       py = R[3] * x0 + R[4] * y0 + R[5] * z0 + p[1];
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
-    }
-    const float el2 = ex * ex + ey * ey + ez * ez;
-    cfloat* ber = (cfloat*)B.er;
-#pragma unroll 4
-    for (int k = B.e0; k < B.e1; ++k) {
-      cfloat* E = ber + 16 * k;
-      const float cx = E[0], cy = E[1], cz = E[2], dx = E[3], dy = E[4], dz = E[5];
-      const float cba = cx * ux + cy * uy + cz * uz;
-      const float dba = dx * ux + dy * uy + dz * uz;
-      if (valid && cba * dba < 0.f) {
-        const float wx = E[6], wy = E[7], wz = E[8];
-        const float adc = ax * wx + ay * wy + az * wz;
-        const float bdc = bx * wx + by * wy + bz * wz;
-        if (adc * bdc < 0.f && cba * bdc > 0.f) {
-          const float fx = E[9], fy = E[10], fz = E[11];
-          float n0 = ey * fz - ez * fy, n1 = ez * fx - ex * fz, n2 = ex * fy - ey * fx;
-          const float len2 = n0 * n0 + n1 * n1 + n2 * n2;
-          const float fl2 = fx * fx + fy * fy + fz * fz;
-          if (!(len2 > 1e-4f * el2 * fl2)) {
-            deg = true;  // nearly parallel (or degenerate) edges: the axis needs fp64
-          } else {
-            const float il = rsqrtf(len2);
-            const float ori = n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz);
-            deg |= fabsf(ori) * il < 1e-4f;
-            if (ori < 0.f) { n0 = -n0; n1 = -n1; n2 = -n2; }
-            const float ov = n0 * (px - E[12]) + n1 * (py - E[13]) + n2 * (pz - E[14]);
-            loc = fminf(loc, ov * il);
+    };
+    unsigned cm = 0;  // pass 1: bit k = cluster c0 + k may hold an arc crossing this lane's
+    {
+      const int e = base + lane;
+      if (e < A.e1) {
+        const ushort4 ix = A.ei[e];
+        const float4 na = A.pl[ix.z], nb = A.pl[ix.w];
+        // the arc's cone in A's frame, its axis rotated into the world
+        const float sx = na.x + nb.x, sy = na.y + nb.y, sz = na.z + nb.z;
+        const float s2 = sx * sx + sy * sy + sz * sz;
+        if (!(s2 > 1e-6f)) {
+          cm = nC >= 32 ? 0xffffffffu : ((1u << nC) - 1u);  // a knife edge: no cone
+        } else {
+          const float is = rsqrtf(s2);
+          const float qx = (R[0] * sx + R[1] * sy + R[2] * sz) * is;
+          const float qy = (R[3] * sx + R[4] * sy + R[5] * sz) * is;
+          const float qz = (R[6] * sx + R[7] * sy + R[8] * sz) * is;
+          const float cab = na.x * nb.x + na.y * nb.y + na.z * nb.z;
+          const float ca = sqrtf(fmaxf(0.f, 0.5f * (1.f + cab))),
+                      sa = sqrtf(fmaxf(0.f, 0.5f * (1.f - cab)));
+          const float4* cl = B.cl + 2 * B.c0;
+          for (int k = 0; k < nC; ++k) {
+            const float4 c = cl[2 * k], s = cl[2 * k + 1];
+            // the cones overlap iff angle(axes) <= half_a + half_b: always when that sum
+            // reaches pi (half_b >= pi - half_a, i.e. cos half_b <= -cos half_a; half_a <=
+            // pi / 2), else cos(angle) >= cos(half_a + half_b), less the slack
+            if (c.w <= -ca + kConeSlack ||
+                qx * c.x + qy * c.y + qz * c.z >= ca * c.w - sa * s.x - kConeSlack)
+              cm |= 1u << k;
           }
         }
       }
     }
-    if (base + 64 < A.e1 && !__ballot(deg)) {
-      const float lf = fminf(pd, wave_minf(loc));
-      if (lf < stop) { if (STAT) TCMP_MSTAT(10); return lf; }
+    const int cnt = __builtin_popcount(cm);
+    int pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(pre, o);
+      if (lane >= o) pre += t;
+    }
+    const int total = __shfl(pre, 63);
+    pre -= cnt;  // lane l's candidates are ranks [pre, pre + cnt)
+    for (int w0 = 0; w0 < total; w0 += 64) {
+      const int w = w0 + lane;
+      int src = 0;  // the last lane whose prefix is <= w
+#pragma unroll
+      for (int step = 32; step; step >>= 1)
+        if (__shfl(pre, src + step) <= w) src += step;
+      unsigned m = (unsigned)__shfl((int)cm, src);
+      const int kk = w - __shfl(pre, src);
+      if (w < total) {
+        for (int j = 0; j < kk; ++j) m &= m - 1;
+        const float4 cs = B.cl[2 * (B.c0 + __builtin_ctz(m)) + 1];
+        const int r0 = __float_as_int(cs.y), r1 = __float_as_int(cs.z);
+        float ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz;
+        a_edge(base + src, ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz);
+        const float el2 = ex * ex + ey * ey + ez * ez;
+        for (int k = r0; k < r1; ++k) {
+          const float4* E4 = reinterpret_cast<const float4*>(B.er + 16 * k);
+          const float4 r0v = E4[0], r1v = E4[1];  // c (x y z), d (x | y z), w (x y)
+          const float cba = r0v.x * ux + r0v.y * uy + r0v.z * uz;
+          const float dba = r0v.w * ux + r1v.x * uy + r1v.y * uz;
+          if (cba * dba < 0.f) {
+            const float4 r2v = E4[2], r3v = E4[3];  // w z | edge vector | endpoint x, endpoint y z
+            const float wx = r1v.z, wy = r1v.w, wz = r2v.x;
+            const float adc = ax * wx + ay * wy + az * wz;
+            const float bdc = bx * wx + by * wy + bz * wz;
+            if (adc * bdc < 0.f && cba * bdc > 0.f) {
+              const float fx = r2v.y, fy = r2v.z, fz = r2v.w;
+              float n0 = ey * fz - ez * fy, n1 = ez * fx - ex * fz, n2 = ex * fy - ey * fx;
+              const float len2 = n0 * n0 + n1 * n1 + n2 * n2;
+              const float fl2 = fx * fx + fy * fy + fz * fz;
+              if (!(len2 > 1e-4f * el2 * fl2)) {
+                deg = true;  // nearly parallel (or degenerate) edges: the axis needs fp64
+              } else {
+                const float il = rsqrtf(len2);
+                const float ori = n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz);
+                deg |= fabsf(ori) * il < 1e-4f;
+                if (ori < 0.f) { n0 = -n0; n1 = -n1; n2 = -n2; }
+                const float ov = n0 * (px - r3v.x) + n1 * (py - r3v.y) + n2 * (pz - r3v.z);
+                loc = fminf(loc, ov * il);
+              }
+            }
+          }
+        }
+      }
+      if ((w0 + 64 < total || base + 64 < A.e1) && !__ballot(deg)) {
+        const float lf = fminf(pd, wave_minf(loc));
+        if (lf < stop) { if (STAT) TCMP_MSTAT(10); return lf; }
+      }
     }
   }
   if (__ballot(deg)) { if (STAT) TCMP_MSTAT(13); return __builtin_nanf(""); }
