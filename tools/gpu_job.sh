@@ -4,6 +4,7 @@
 # stages:
 #   tests[=K]        pytest -m gpu (optionally -k K), then smoke()
 #   bench[=W]        bench.py line for workload W (c3 default), 5 steps (c5: 2)
+#   default          the driver's own default command, `python bench.py` (C3, CPU baseline too)
 #   trace[=W]        rocprofv3 --kernel-trace --stats of the same bench command
 #   pmc[=W]          PMC passes FETCH_SIZE / WRITE_SIZE (one run each) over one bench step
 #   sq[=W]           PMC pass of SQ wave / busy counters over one bench step
@@ -41,6 +42,8 @@ for st in "$@"; do
     bench)
       w=${arg:-c3}
       timeout -k 10 300 python -u bench.py $(bench_args $w) > $O/bench_$w.json 2> $O/bench_$w.err ;;
+    default)
+      timeout -k 10 600 python -u bench.py > $O/bench_default.json 2> $O/bench_default.err ;;
     trace)
       w=${arg:-c3}
       timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace_$w -o run --output-format csv \
