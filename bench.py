@@ -487,7 +487,8 @@ def main():
                               "value keeps %d queries in flight" % pipe}
         barrier()
     kernel_ms = {k: sum(x[k] for x in kres) / S for k in
-                 ("ms_nearest", "ms_nn_scan", "ms_edges", "ms_insert", "ms_rewire", "ms_finish")}
+                 ("ms_nearest", "ms_nn_scan", "ms_edge_prep", "ms_edges", "ms_insert", "ms_rewire",
+                  "ms_finish")}
     if args.verbose and rank == 0:
         print(json.dumps({"per_step": results, "kernel_ms_per_step": kernel_ms}), file=sys.stderr)
     launches = sum(x["launches_nearest"] for x in kres)  # one k_edges launch per round

@@ -231,6 +231,8 @@ typedef struct {
                              engine's lanes */
   uint64_t rewire_steps;  /* the rewire edges' extend steps (part of edge_steps, not k_edges') */
   int64_t graph_launches; /* tcmp_plan_run calls of this plan replayed as one captured graph */
+  double ms_edge_prep;    /* the edge order's sort and work records before k_edges (ms_edges
+                             times k_edges alone) */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the

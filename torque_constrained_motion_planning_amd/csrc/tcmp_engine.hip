@@ -1153,7 +1153,9 @@ struct DBuf {
 };
 
 // F_NNSCAN times the k_nearest_wave launch alone (inside F_NEAREST, not added to totals)
-enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_NNSCAN, F_COUNT };
+// F_EDGE_PREP: the edge order's counting sort and k_edge_records, so that F_EDGES times
+// k_edges alone (its roofline divides by that time)
+enum Fam { F_NEAREST = 0, F_EDGES, F_INSERT, F_REWIRE, F_FINISH, F_NNSCAN, F_EDGE_PREP, F_COUNT };
 
 // one family's span between two recorded events; adjacent families share the boundary event
 // (one record per boundary: each record is an event node of ~5 us in a round graph)
@@ -1666,7 +1668,9 @@ __global__ __launch_bounds__(256) void k_edge_order_keys(const PlanParams* __res
 }
 
 // reset_counter = false: the plan's k_nn_home already cleared the work counter
-int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool reset_counter = true) {
+// kernel_begin (nullable): an event recorded between k_edge_records and k_edges (timing on)
+int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool reset_counter = true,
+                 hipEvent_t* kernel_begin = nullptr) {
   if (J.n <= 0) return 0;
   if (reset_counter) HIPCHK(hipMemsetAsync(&h->st->work_counter, 0, sizeof(int), h->stream));
   // persistent grid bounded by residency (256-thread blocks hold one wave per SIMD each).
@@ -1686,6 +1690,7 @@ int launch_edges(tcmp_handle* h, const EdgeJob& J, const PlanParams* dP, bool re
   if (split > 1) blocks = std::min(cap, ((long long)split * J.n + 255) / 256);
   h->edge_blocks = (int)blocks;
   hipLaunchKernelGGL(k_edge_records, dim3(grid_for(J.n, 256)), dim3(256), 0, h->stream, J, dP);
+  if (kernel_begin) *kernel_begin = h->mark();
   const bool mk = h->mesh_kernels();
   auto kern = split == 4 ? (mk ? k_edges<true, 4> : k_edges<false, 4>)
               : split == 2 ? (mk ? k_edges<true, 2> : k_edges<false, 2>)
@@ -2993,8 +2998,10 @@ static int round_search(tcmp_handle* h, bool device_samples, int32_t nb, long lo
   // k_edges counts the accepted edges per 256 lanes (bcount, cleared by the nearest search's
   // first kernel); the scan turns them into the insertion offsets
   J.accepted = h->bcount.p;
-  if (int rc = launch_edges(h, J, h->dP, false)) return rc;
-  h->ins_ev = h->mark_end(F_EDGES, e1);
+  hipEvent_t ek = nullptr;
+  if (int rc = launch_edges(h, J, h->dP, false, &ek)) return rc;
+  h->span(F_EDGE_PREP, e1, ek);
+  h->ins_ev = h->mark_end(F_EDGES, ek);
   hipLaunchKernelGGL(k_ins_scan, dim3(1), dim3(1024), 0, h->stream, h->st, h->bcount.p, nblk,
                      h->boff.p);
   HIPCHK(hipGetLastError());
@@ -3480,6 +3487,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   r->launches_nn_scan = h->launches_scan;
   r->nn_box_tests = s.nn_box_tests;
   r->ms_nn_scan = h->ms[F_NNSCAN];
+  r->ms_edge_prep = h->ms[F_EDGE_PREP];
   r->snap_sum = s.snap_sum;
   r->nn_full_pairs = s.nn_full_pairs;
   r->n_rewires = s.rewires;
