@@ -110,10 +110,11 @@ WORKLOADS = {
                     "(queries_in_flight of them planned concurrently; config_single_query = one "
                     "at a time)"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
-               queries=64, scaling="strong", pipeline=2,
+               queries=64, scaling="strong", pipeline=2, fleet=8,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
                     "samples each) per step, sharded round-robin over the GPUs, solved paths "
-                    "gathered to rank 0 over RCCL"),
+                    "gathered to rank 0 over RCCL; a GPU's queries grow their trees in fused "
+                    "rounds, `fleet` queries per set of kernel launches"),
     "c5": dict(boxes=0, meshes=256, mode=_lib.TORQUE_RNE, mass=5.0, samples=10_000_000,
                batch=262144, queries=1, scaling="strong", pipeline=2,
                text="C5: dense clutter, 256 convex meshes (Panda link hulls scaled 0.5-1.5, "
@@ -199,6 +200,30 @@ def run_query(eng, obs, goal, n_samples, batch, seed, mode=_lib.TORQUE_RNE, mass
         for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
             HOST_MS[k] += (b - a) * 1e3
     return r, out
+
+
+def run_fleet(engs, qs, n_samples, batch, seeds, mode=_lib.TORQUE_RNE, mass=5.0, exec_time=5.0):
+    """len(qs) independent queries (each its own scene, goal and seed) as one fleet: begin each
+    plan on its own engine, grow every tree in fused rounds (tcmp_plan_run_fused: one set of
+    kernel launches per round for all of them), then finish and fetch each plan."""
+    t0 = time.perf_counter()
+    for e, (obs, pack, goal), seed in zip(engs, qs, seeds):
+        e.set_scene(obs, pack)
+        st = e.plan_begin(START, goal, mode, mass, exec_time, max_nodes=n_samples + 1,
+                          max_batch=batch, seed=seed)
+        if st != _lib.PLAN_OK:
+            raise RuntimeError("start/goal in collision")
+    t1 = time.perf_counter()
+    _lib.plan_run_fused(engs[:len(qs)], n_samples, batch)
+    t2 = time.perf_counter()
+    rs = [e.plan_finish() for e in engs[:len(qs)]]
+    t3 = time.perf_counter()
+    outs = [e.plan_fetch(r) if r.goal_found else None for e, r in zip(engs, rs)]
+    t4 = time.perf_counter()
+    with HOST_MS_LOCK:
+        for k, a, b in (("begin", t0, t1), ("run", t1, t2), ("finish", t2, t3), ("fetch", t3, t4)):
+            HOST_MS[k] += (b - a) * 1e3
+    return list(zip(rs, outs))
 
 
 def usable_cores():
@@ -303,6 +328,9 @@ def main():
     ap.add_argument("--streams", type=int, default=None,
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
+    ap.add_argument("--fleet", type=int, default=None,
+                    help="queries per fused round (tcmp_plan_run_fused) when a rank plans several "
+                         "queries per step (default 8 for c4; 0 or 1: one engine per query)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
@@ -375,17 +403,29 @@ def main():
     # with --pipeline P run P consecutive steps at once the same way (step s on engine s mod P).
     pipe = max(1, args.pipeline if args.pipeline is not None else W.get("pipeline", 1)) \
         if not shared else 1
-    n_streams = max(1, min(len(queries) * pipe, args.streams if args.streams else 16))
-    engines = [eng] + [_lib.Engine(gpu) for _ in range(n_streams - 1)]
+    fleet = args.fleet if args.fleet is not None else W.get("fleet", 0)
+    fleet = min(fleet, len(queries)) if len(queries) > 1 and not shared else 0
+    if fleet > 1:
+        # fleets of `fleet` queries, `pipe` of them in flight (a group of engines each)
+        fleets = [list(range(f, min(f + fleet, len(queries)))) for f in range(0, len(queries), fleet)]
+        n_streams = max(1, min(len(fleets) * pipe, args.streams if args.streams else pipe))
+        n_engines = n_streams * fleet
+    else:
+        fleets = None
+        n_streams = max(1, min(len(queries) * pipe, args.streams if args.streams else 16))
+        n_engines = n_streams
+    engines = [eng] + [_lib.Engine(gpu) for _ in range(n_engines - 1)]
     for e in engines[1:]:
         e.set_self_collision(args.self_collisions)
     pool = None
     if n_streams > 1:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(n_streams)
+    if n_engines > 1:
         # concurrent queries: no per-family event timing (an overlapped launch's span includes
-        # its neighbours' kernels, and the round graphs then hold kernel nodes only); the
-        # per-kernel figures come from the one-at-a-time pass after the timed region
+        # its neighbours' kernels, and the round graphs then hold kernel nodes only; fused
+        # rounds record none); the per-kernel figures come from the one-at-a-time pass after
+        # the timed region
         for e in engines:
             e.set_timing(False)
 
@@ -404,6 +444,14 @@ def main():
                 if idx is None:
                     return got
                 j, s = jobs[idx]
+                if fleets is not None:
+                    # job j = fleet j of step s on this thread's group of engines
+                    qs = fleets[j]
+                    done = run_fleet(engines[k * fleet:(k + 1) * fleet], [queries[i] for i in qs],
+                                     W["samples"], W["batch"],
+                                     [step_seed(s) + 7919 * i for i in qs], mode, mass)
+                    got += [(idx * fleet + t, s) + d for t, d in enumerate(done)]
+                    continue
                 obs, pack, goal = queries[j]
                 got.append((idx, s) + run_query(engines[k], obs, goal, W["samples"], W["batch"],
                                                 step_seed(s) + 7919 * j, mode, mass, meshes=pack,
@@ -412,7 +460,8 @@ def main():
                       key=lambda x: x[0])
 
     def step_group(ss):
-        done = run_jobs([(j, s) for s in ss for j in range(len(queries))])
+        done = run_jobs([(j, s) for s in ss
+                         for j in range(len(fleets) if fleets is not None else len(queries))])
         res = []
         for s in ss:
             part = [d for d in done if d[1] == s]
@@ -465,7 +514,7 @@ def main():
     # one-query-at-a-time throughput (config_single_query), same build, same box.
     kres = results
     single = None
-    if n_streams > 1:
+    if n_engines > 1:
         e0 = engines[0]
         e0.set_timing(True)
         obs, pack, goal = queries[0]
@@ -587,8 +636,10 @@ def main():
                    "samples_per_query": W["samples"], "queries_per_step": n_queries_total,
                    "batch_per_round": W["batch"], "execution_time_s": 5.0,
                    "parallelism": ("shared-tree x%d" if shared else "query-sharded x%d") % world,
-                   "streams_per_gpu": n_streams, "pipelined_steps": pipe,
-                   "queries_in_flight": min(n_streams, len(queries) * pipe),
+                   "streams_per_gpu": n_engines, "pipelined_steps": pipe,
+                   "queries_in_flight": (min(n_streams * fleet, len(queries) * pipe) if fleets
+                                         else min(n_streams, len(queries) * pipe)),
+                   "fused_queries": fleet if fleets else 1,
                    "self_collisions": bool(args.self_collisions)},
         "roofline": dominant,
         "roofline_other": other,
@@ -606,7 +657,7 @@ def main():
         # inside plan_finish's first wait, so "finish" holds most of the step)
         "host_ms_per_step": host_ms,
         "host_ms_note": ("per step, summed over the host threads of the queries in flight"
-                         if n_streams > 1 else "per step"),
+                         if n_engines > 1 else "per step"),
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},

@@ -261,6 +261,16 @@ int tcmp_plan_run_shared(tcmp_handle* h, tcmp_comm* c, int64_t n_samples, int32_
  * tcmp_plan_run_shared (and its parity check on one GPU). */
 int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch);
 
+/* fused multi-plan rounds: n (1..31) engines on one device, each with its own open plan (its
+ * own scene, start, goal, seed), all at the same round, grow their trees together -- one set
+ * of kernel launches per round serves every plan's lanes (tcmp_fleet.h), on hs[0]'s stream;
+ * the other engines' streams are ordered before and after it.  Every plan's tree is
+ * bit-identical to what tcmp_plan_run(hs[q], n_samples, batch) grows alone; finish and fetch
+ * each plan on its own engine as usual.  Box scenes only (no meshes, no self-collision pairs);
+ * the plans must share the distance weights.  The multi-query form of tcmp_plan_run
+ * (collect_data.py:74-85 plans several start/goal queries per scene step). */
+int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch);
+
 /* goal node of the open plan (-1 while none) and its cost -- goal_n.cost, the bound of the
  * informed rejection test (rrt_star.py:163-165); cost may be NULL. */
 int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost);

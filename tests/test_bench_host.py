@@ -82,6 +82,13 @@ def _run_bench(monkeypatch, capsys, argv):
     import bench
     from torque_constrained_motion_planning_amd import _lib
     monkeypatch.setattr(_lib, "Engine", _FakeEngine)
+    _FakeEngine.fused = []
+
+    def fused(engines, n_samples, batch):  # tcmp_plan_run_fused: one call for the fleet
+        _FakeEngine.fused.append(len(engines))
+        engines[0].plan_run(n_samples, batch)
+
+    monkeypatch.setattr(_lib, "plan_run_fused", fused)
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)
@@ -117,11 +124,31 @@ def test_bench_pipelined_single_query_steps(monkeypatch, capsys, pipe):
     assert line["stats_last_step"]["status"] == 0
 
 
+def test_bench_fused_fleets(monkeypatch, capsys):
+    """c4's default: a step's queries in fleets (fused rounds), `pipeline` fleets in flight,
+    each on its own group of engines; every query still begins, finishes and is fetched on its
+    own engine with its own seed."""
+    line = _run_bench(monkeypatch, capsys, ["--workload", "c4", "--queries", "6", "--steps", "2",
+                                            "--warmup", "1", "--pipeline", "2", "--fleet", "3",
+                                            "--no-cpu-baseline"])
+    c = line["config"]
+    assert c["queries_per_step"] == 6 and c["fused_queries"] == 3
+    assert c["streams_per_gpu"] == 6 and c["queries_in_flight"] == 6
+    # two fleets per step: warmup 2 steps + 2 timed steps -> 8 fused calls of 3 plans
+    assert _FakeEngine.fused == [3] * 8
+    assert _FakeEngine.peak == 2  # two fleets in flight
+    # 4 steps x 6 queries + (1 warmup + 2) one-at-a-time kernel-timing queries, seeds distinct
+    assert len(_FakeEngine.seeds) == 27 and len(set(_FakeEngine.seeds)) == 27
+    assert line["value"] == pytest.approx(6 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)
+    assert "one at a time" in line["kernel_timing"]
+
+
 def test_bench_multi_query_pipeline(monkeypatch, capsys):
     line = _run_bench(monkeypatch, capsys, ["--workload", "c4", "--queries", "3", "--steps", "2",
-                                            "--warmup", "1", "--pipeline", "2",
+                                            "--warmup", "1", "--pipeline", "2", "--fleet", "0",
                                             "--no-cpu-baseline"])
-    assert line["config"]["queries_per_step"] == 3
+    assert line["config"]["queries_per_step"] == 3 and line["config"]["fused_queries"] == 1
+    assert _FakeEngine.fused == []
     assert line["config"]["streams_per_gpu"] == 6  # 3 queries x 2 steps in flight
     assert "one at a time" in line["kernel_timing"] and "config_single_query" not in line
     assert line["config"]["queries_in_flight"] == 6

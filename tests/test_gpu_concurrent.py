@@ -99,3 +99,23 @@ def test_concurrent_graph_capture_then_replay(n_obs, n_mesh, n, batch):
         assert ms[1] == 0.0 and ms[0] > 0.0 and ms[2] > 0.0, ms
     for e in engines:
         e.close()
+
+
+def test_plan_run_shape_change_keeps_event_spans():
+    """plan_run(n1, B) then plan_run(n2, B) on one engine: the second call captures a new
+    round graph and destroys the first one's event nodes -- their spans must have been read
+    first (this sequence aborted in the HIP runtime at plan_finish before the fix), and the
+    per-family times keep counting both calls."""
+    import bench
+    from torque_constrained_motion_planning_amd import _lib
+    eng = _lib.Engine(0)
+    obs, pack, goal = bench.make_query(4343, n_obs=12, mode=2, mass=5.0, engine=eng)
+    eng.set_scene(obs)
+    assert eng.plan_begin(bench.START, goal, 2, 5.0, 5.0, max_nodes=17_001, max_batch=4608,
+                          seed=3) == _lib.PLAN_OK
+    eng.plan_run(10_000, 4608)
+    eng.plan_run(7_000, 4608)
+    r = eng.plan_finish()
+    assert r.n_samples == 17_000 and r.n_nodes > 1000
+    assert r.ms_edges > 0 and r.ms_nearest > 0 and r.graph_launches == 2
+    eng.close()

@@ -29,7 +29,7 @@ EXPORTS = [
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_retrace",
-    "tcmp_plan_run_shared", "tcmp_plan_run_group",
+    "tcmp_plan_run_shared", "tcmp_plan_run_group", "tcmp_plan_run_fused",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_digest", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters", "tcmp_microbench",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
@@ -132,6 +132,9 @@ def load_library(path=LIB_PATH):
         L.tcmp_plan_run_group.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.c_int64,
                                           ctypes.c_int32]
         L.tcmp_plan_run.argtypes = [vp, ctypes.c_int64, ctypes.c_int32]
+        if hasattr(L, "tcmp_plan_run_fused"):  # absent from A/B builds of older sources
+            L.tcmp_plan_run_fused.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.c_int64,
+                                              ctypes.c_int32]
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_retrace.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
@@ -618,6 +621,19 @@ def plan_run_group(engines, n_samples, batch):
     arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
     L = load_library()
     rc = L.tcmp_plan_run_group(arr, len(engines), int(n_samples), int(batch))
+    if rc != 0:
+        raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
+
+
+def plan_run_fused(engines, n_samples, batch):
+    """tcmp_plan_run_fused: the open plans of several engines (one device, each its own scene,
+    start, goal and seed, all at the same round) grow their trees in fused rounds -- one set of
+    kernel launches per round for all of them.  Each engine ends with the tree its own
+    plan_run(n_samples, batch) grows; finish and fetch each plan on its own engine."""
+    engines = list(engines)
+    arr = (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+    L = load_library()
+    rc = L.tcmp_plan_run_fused(arr, len(engines), int(n_samples), int(batch))
     if rc != 0:
         raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
 

@@ -204,10 +204,11 @@ __device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long x)
 // ------------------------------------------------------------------------------------------
 // k_sample: uniform configurations (utils.py:2941-2990 convex_combination of the limits)
 // ------------------------------------------------------------------------------------------
-__global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long long base, int nb, double* cand,
-                         unsigned char* cgoal) {
+// (lane j of the round; the fused multi-plan rounds of tcmp_fleet.h call the same body)
+__device__ __forceinline__ void sample_lane(const PlanParams* __restrict__ Pd, DevState* st,
+                                            long long base, int nb, double* cand,
+                                            unsigned char* cgoal, int j) {
   const PlanParams P = *Pd;
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= nb) return;
   const long long it = base + j;
   double u[8];
@@ -235,6 +236,10 @@ __global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long l
   const bool raw = it == 0 || u[7] < P.goal_prob;
   const uint64_t m = __ballot(raw);
   if (m && lane == __builtin_ctzll(m)) atomicMin(&st->round_goal, j);
+}
+__global__ void k_sample(const PlanParams* __restrict__ Pd, DevState* st, long long base, int nb,
+                         double* cand, unsigned char* cgoal) {
+  sample_lane(Pd, st, base, nb, cand, cgoal, blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -352,7 +357,7 @@ __global__ __launch_bounds__(256) void k_cs_hist(const int* bin, int n, int nbin
   }
 }
 // one block: hoff = exclusive scan of hist, hist zeroed
-__global__ __launch_bounds__(1024) void k_cs_scan(int* hist, int nbins, int* hoff) {
+__device__ __forceinline__ void cs_scan_block(int* hist, int nbins, int* hoff) {
   __shared__ int part[1024];
   const int t = threadIdx.x;
   const int per = (nbins + 1023) / 1024, b0 = t * per, b1 = min(nbins, b0 + per);
@@ -374,12 +379,15 @@ __global__ __launch_bounds__(1024) void k_cs_scan(int* hist, int nbins, int* hof
     hist[b] = 0;
   }
 }
+__global__ __launch_bounds__(1024) void k_cs_scan(int* hist, int nbins, int* hoff) {
+  cs_scan_block(hist, nbins, hoff);
+}
 // perm[hoff[bin] + rank] = item; with few bins each block reserves its range per bin once
-__global__ __launch_bounds__(256) void k_cs_scatter(const int* bin, int n, int nbins, int* hoff,
-                                                    int* perm) {
+__device__ __forceinline__ void cs_scatter_block(const int* bin, int n, int nbins, int* hoff,
+                                                 int* perm, int blk) {
   __shared__ int lc[kCsLdsBins];
   const bool lds = nbins <= kCsLdsBins;
-  const int i = blockIdx.x * 256 + threadIdx.x;
+  const int i = blk * 256 + threadIdx.x;
   const int b = i < n ? bin[i] : 0;
   if (!lds) {
     if (i < n) perm[atomicAdd(&hoff[b], 1)] = i;
@@ -393,6 +401,10 @@ __global__ __launch_bounds__(256) void k_cs_scatter(const int* bin, int n, int n
     if (lc[k]) lc[k] = atomicAdd(&hoff[k], lc[k]);
   __syncthreads();
   if (i < n) perm[lc[b] + r] = i;
+}
+__global__ __launch_bounds__(256) void k_cs_scatter(const int* bin, int n, int nbins, int* hoff,
+                                                    int* perm) {
+  cs_scatter_block(bin, n, nbins, hoff, perm, blockIdx.x);
 }
 
 #include "tcmp_nn.h"
@@ -427,8 +439,8 @@ struct EdgeJob {
 // and its planned step count num_steps(from, to[e]) (utils.py:3072).  A fetch is then one
 // dependent load after the work counter, where it was three (order, from_idx, the rows) and a
 // num_steps on the wave-step that fetched.
-__global__ __launch_bounds__(256) void k_edge_records(EdgeJob J, const PlanParams* __restrict__ Pd) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+__device__ __forceinline__ void edge_record(const EdgeJob& J, const PlanParams* __restrict__ Pd,
+                                            int k) {
   if (k >= J.n) return;
   const int e = J.order ? J.order[k] : k;
   const long long src = J.from_idx ? (long long)J.from_idx[e] : (long long)e;
@@ -441,6 +453,9 @@ __global__ __launch_bounds__(256) void k_edge_records(EdgeJob J, const PlanParam
   double* r = J.rec + 8 * (size_t)k;
   *reinterpret_cast<double4*>(r) = make_double4(a[0], a[1], a[2], a[3]);
   *reinterpret_cast<double4*>(r + 4) = make_double4(a[4], a[5], a[6], __hiloint2double(n, e));
+}
+__global__ __launch_bounds__(256) void k_edge_records(EdgeJob J, const PlanParams* __restrict__ Pd) {
+  edge_record(J, Pd, blockIdx.x * 256 + threadIdx.x);
 }
 
 #ifndef TCMP_EDGE_SPLIT
@@ -456,6 +471,7 @@ __global__ __launch_bounds__(256) void k_edge_records(EdgeJob J, const PlanParam
 // ends at the first failing step, exactly the sequential walk's result; the checks past a
 // failure are wasted only in an edge's last iteration.  The counted extend steps are the
 // sequential walk's (nsafe + 1 on a failure, else n).
+
 template <bool MESH, int SPLIT>
 __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const PlanParams* __restrict__ Pd, Scene sc_g, Geo g_g,
                                                DevState* st) {
@@ -625,16 +641,17 @@ __global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_edges(EdgeJob J, const 
 // rewire (rrt_star.py:183-192): neighbours of each new node within `radius` among the
 // round's snapshot, visited in index order; reparent when cheaper and the edge is safe.
 // ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_rewire_scan(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
-                                                     const int* rwlist, int* nbr, int* ncount) {
+__device__ __forceinline__ void rewire_scan_block(const PlanParams* __restrict__ Pd, DevState* st,
+                                                  const Tree& tr, const int* rwlist, int* nbr,
+                                                  int* ncount, int blk) {
   const PlanParams P = *Pd;
   // neighbours within `radius` of each flagged new node among the snapshot, in index order
   // (the order rrt_star.py:187 visits them); the snapshot streams through LDS tiles
   __shared__ double4 tile[2 * kNnTile];
   const int tid = threadIdx.x;
   const long long R = st->rw_count, T = st->snap;
-  if ((long long)blockIdx.x * 256 >= R) return;  // block-uniform
-  const long long t = (long long)blockIdx.x * 256 + tid;
+  if ((long long)blk * 256 >= R) return;  // block-uniform
+  const long long t = (long long)blk * 256 + tid;
   const bool act = t < R;
   double qn[7];
   if (act) load7(tr.cfg + 8 * (long long)rwlist[t], qn);
@@ -669,18 +686,23 @@ __global__ __launch_bounds__(256) void k_rewire_scan(const PlanParams* __restric
   }
   if (act) ncount[t] = c;
 }
+__global__ __launch_bounds__(256) void k_rewire_scan(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
+                                                     const int* rwlist, int* nbr, int* ncount) {
+  rewire_scan_block(Pd, st, tr, rwlist, nbr, ncount, blockIdx.x);
+}
 
 template <bool MESH>
-__global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
-                                                      const int* rwlist, const int* nbr,
-                                                      const int* ncount, Scene sc_g, Geo g_g) {
+__device__ __forceinline__ void rewire_apply_block(const PlanParams* __restrict__ Pd, DevState* st,
+                                                   const Tree& tr, const int* rwlist,
+                                                   const int* nbr, const int* ncount,
+                                                   const Scene& sc_g, const Geo& g_g, int blk) {
   const PlanParams P = *Pd;
   extern __shared__ double tcmp_lds[];
   Scene sc;
   Geo g;
   stage_lds<!MESH>(sc_g, g_g, tcmp_lds, sc, g);
   const long long R = st->rw_count, T = st->snap;
-  const long long t = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long t = (long long)blk * blockDim.x + threadIdx.x;
   const bool act = t < R && ncount[t] > 0;
   if (__ballot(act) == 0) return;  // wave-uniform
   const long long me = act ? rwlist[t] : 0;
@@ -773,6 +795,12 @@ __global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restri
     atomicAdd(&st->edge_steps, sn);
     atomicAdd(&st->rewire_steps, sn);
   }
+}
+template <bool MESH>
+__global__ __launch_bounds__(256) void k_rewire_apply(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
+                                                      const int* rwlist, const int* nbr,
+                                                      const int* ncount, Scene sc_g, Geo g_g) {
+  rewire_apply_block<MESH>(Pd, st, tr, rwlist, nbr, ncount, sc_g, g_g, blockIdx.x);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1291,6 +1319,14 @@ struct tcmp_handle {
   long long launches_nearest = 0;
   long long launches_scan = 0;      // k_nearest_wave32 launches of the open plan
   int edge_blocks = 0;
+  // fused multi-plan rounds (tcmp_plan_run_fused, tcmp_fleet.h) led by this engine: the plan
+  // descriptors (FleetPlan[K], FleetNN[K]), each plan's first row in the fleet's node index,
+  // and the event the other engines' streams wait on.  The fleet's index lives in this
+  // engine's index buffers and st_nn.
+  DBuf<unsigned char> f_desc;
+  DBuf<long long> f_off;
+  std::vector<unsigned char> f_host;
+  hipEvent_t dep_ev = nullptr;
   int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
   int edge_wps = 2;    // k_edges' persistent grid, blocks per CU (environment TCMP_EDGE_WPS=1/2)
 
@@ -1493,10 +1529,10 @@ int ensure_index(tcmp_handle* h, size_t N, size_t B) {
 
 // the first round: nearest = the root, score = its exact score (the scan's arithmetic), second
 // bound +inf; also the resets k_nn_home does for the scan and the edge kernel
-__global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const double* cfg,
-                          const double* cand, int nb, int* nn, double* second, double* score,
-                          GoalFix gf, int* bcount) {
-  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void nn_root_lane(const PlanParams* __restrict__ Pd, DevState* st,
+                                             const double* cfg, const double* cand, int nb, int* nn,
+                                             double* second, double* score, GoalFix gf,
+                                             int* bcount, int j) {
   if (j < 8) st->nn_queue[j] = 0;
   if (j == 0) {
     st->nn_counter = 0;
@@ -1530,6 +1566,12 @@ __global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const
   nn[j] = 0;
   if (second) second[j] = INFINITY;
   if (score) score[j] = dd;
+}
+__global__ void k_nn_root(const PlanParams* __restrict__ Pd, DevState* st, const double* cfg,
+                          const double* cand, int nb, int* nn, double* second, double* score,
+                          GoalFix gf, int* bcount) {
+  nn_root_lane(Pd, st, cfg, cand, nb, nn, second, score, gf, bcount,
+               blockIdx.x * blockDim.x + threadIdx.x);
 }
 
 // Exact nearest node of nb candidates (rows of 8) among the st->n_nodes <= T_bound tree rows
@@ -1647,13 +1689,13 @@ int launch_nearest(tcmp_handle* h, const PlanParams& P, const PlanParams* dP, De
 // for longest-first scheduling of k_edges
 constexpr int kEdgeOrderMin = 4096;
 // (the counting sort's histogram is built here too: one launch fewer)
-__global__ __launch_bounds__(256) void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg,
-                                                         const int* nn, const double* cand, int nb,
-                                                         int* bins, int* hist) {
+__device__ __forceinline__ void edge_order_block(const PlanParams* __restrict__ Pd, const double* cfg,
+                                                 const int* nn, const double* cand, int nb,
+                                                 int* bins, int* hist, int blk) {
   __shared__ int lh[256];
   lh[threadIdx.x] = 0;
   __syncthreads();
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int e = blk * blockDim.x + threadIdx.x;
   if (e < nb) {
     double a[7], b[7];
     load7(cfg + 8 * (size_t)nn[e], a);
@@ -1665,6 +1707,11 @@ __global__ __launch_bounds__(256) void k_edge_order_keys(const PlanParams* __res
   }
   __syncthreads();
   if (lh[threadIdx.x]) atomicAdd(&hist[threadIdx.x], lh[threadIdx.x]);
+}
+__global__ __launch_bounds__(256) void k_edge_order_keys(const PlanParams* __restrict__ Pd, const double* cfg,
+                                                         const int* nn, const double* cand, int nb,
+                                                         int* bins, int* hist) {
+  edge_order_block(Pd, cfg, nn, cand, nb, bins, hist, blockIdx.x);
 }
 
 // reset_counter = false: the plan's k_nn_home already cleared the work counter
@@ -1889,6 +1936,9 @@ int tcmp_destroy(tcmp_handle* h) {
                   &h->i1, &h->i2, &h->rwlist})
     b->release();
   h->nnscore.release();
+  h->f_desc.release();
+  h->f_off.release();
+  if (h->dep_ev) (void)hipEventDestroy(h->dep_ev);
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
   h->cs_hist.release();
   h->cs_hoff.release();
@@ -3353,6 +3403,14 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
     // dispatching.  Nothing may allocate or free meanwhile (DBuf::ensure
     // refuses): the graph would bake in a pointer freed under it.
     int rc = 0;
+    // The graph of another shape may still be running, and its event nodes' spans wait in
+    // ev_used for the next collect_events: the stream drains and the spans are read before
+    // the graph and its events are destroyed (plan_run(n1, B) then plan_run(n2, B) on one
+    // engine aborted in the HIP runtime, reading the destroyed events at plan_finish).
+    if (h->rg.exec) {
+      if (int rc_s = sync_stream(h)) return rc_s;
+      h->collect_events();
+    }
     {
       CaptureScope excl;
       h->drop_graph();
@@ -3654,3 +3712,5 @@ int tcmp_plan_debug_round(tcmp_handle* h, int64_t cap, double* cand, int32_t* nn
 }
 
 }  // extern "C"
+
+#include "tcmp_fleet.h"

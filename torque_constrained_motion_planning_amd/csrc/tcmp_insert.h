@@ -8,8 +8,8 @@
 // Included by tcmp_engine.hip after the state types.
 #pragma once
 
-__global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcount, int nblocks,
-                                                   int* boff) {
+__device__ __forceinline__ void ins_scan_block(DevState* st, const int* bcount, int nblocks,
+                                               int* boff) {
   __shared__ int sc[1024];
   const int tid = threadIdx.x;
   int run = 0;
@@ -36,19 +36,23 @@ __global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcou
     st->rw_count = 0;
   }
 }
+__global__ __launch_bounds__(1024) void k_ins_scan(DevState* st, const int* bcount, int nblocks,
+                                                   int* boff) {
+  ins_scan_block(st, bcount, nblocks, boff);
+}
 
-__global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
-                                                   const int* nn, const double* cand,
-                                                   const unsigned char* cgoal, const int* nsafe,
-                                                   const int* nsteps, const double* last, int nb,
-                                                   const int* boff, const double* second,
-                                                   int* rwlist) {
+__device__ __forceinline__ void ins_write_block(const PlanParams* __restrict__ Pd, DevState* st,
+                                                const Tree& tr, const int* nn, const double* cand,
+                                                const unsigned char* cgoal, const int* nsafe,
+                                                const int* nsteps, const double* last, int nb,
+                                                const int* boff, const double* second,
+                                                int* rwlist, int blk) {
   const PlanParams P = *Pd;
   __shared__ int wc[4];
   const long long T = st->n_nodes + st->ins_off;
   if (st->n_nodes + st->ins_all > P.max_nodes) return;  // k_ins_final flags the overflow
   const bool goal_open = st->goal_node < 0;
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int j = blk * 256 + threadIdx.x;
   const bool v = j < nb && nsafe[j] > 0;
   const uint64_t m = __ballot(v);
   const int lane = lane_id(), w = threadIdx.x >> 6;
@@ -57,7 +61,7 @@ __global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict_
   int before = 0;
   for (int i = 0; i < w; ++i) before += wc[i];
   if (!v) return;
-  const long long idx = T + boff[blockIdx.x] + before + (int)__popcll(m & ((1ull << lane) - 1ull));
+  const long long idx = T + boff[blk] + before + (int)__popcll(m & ((1ull << lane) - 1ull));
   const int par = nn[j];
   double pc[7], lq[7], tq[7];
   load7(tr.cfg + 8 * (size_t)par, pc);
@@ -83,8 +87,17 @@ __global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict_
   const double t = sqrt(e2) + r;
   if (second[j] < t * t * (1.0 + 1e-9) + 1e-300) rwlist[atomicAdd(&st->rw_count, 1)] = (int)idx;
 }
+__global__ __launch_bounds__(256) void k_ins_write(const PlanParams* __restrict__ Pd, DevState* st, Tree tr,
+                                                   const int* nn, const double* cand,
+                                                   const unsigned char* cgoal, const int* nsafe,
+                                                   const int* nsteps, const double* last, int nb,
+                                                   const int* boff, const double* second,
+                                                   int* rwlist) {
+  ins_write_block(Pd, st, tr, nn, cand, cgoal, nsafe, nsteps, last, nb, boff, second, rwlist,
+                  blockIdx.x);
+}
 
-__global__ void k_ins_final(const PlanParams* __restrict__ Pd, DevState* st, int nb) {
+__device__ __forceinline__ void ins_final(const PlanParams* __restrict__ Pd, DevState* st, int nb) {
   const PlanParams P = *Pd;
   const long long T = st->n_nodes, total = st->ins_all;
   st->snap = T;
@@ -101,4 +114,7 @@ __global__ void k_ins_final(const PlanParams* __restrict__ Pd, DevState* st, int
   st->snap_sum += (unsigned long long)T;
   st->nn_full_pairs += (unsigned long long)T * (unsigned long long)nb;
   st->round_goal = INT_MAX;
+}
+__global__ void k_ins_final(const PlanParams* __restrict__ Pd, DevState* st, int nb) {
+  ins_final(Pd, st, nb);
 }

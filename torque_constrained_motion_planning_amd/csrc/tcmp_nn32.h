@@ -110,14 +110,28 @@ constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
 // SW: cells per scan round (2 in the engine).  Passing cells queue up across super-cells (the queue
 // holds at most SW) and a round loads all their rows at once: fewer dependent round trips
 // per candidate than one round per super-cell.
-template <bool UW, int SW>
+// FLEET (tcmp_fleet.h): one index over several plans' trees (each plan's nodes a contiguous
+// key range, its cells and super-cells [s0, s1) its own); candidate slot g belongs to plan
+// g / bp, row g % bp of that plan's buffers, and walks only its plan's super-cells.
+struct FleetNN {
+  const double* cand;
+  int* nn;
+  double* second;
+  double* score;
+  DevState* st;   // the plan's counters (nn_pairs, nn_box_tests)
+  int s0, s1;     // the plan's super-cells in this round's index (k_fl_ranges)
+};
+
+template <bool UW, int SW, bool FLEET = false>
 __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const PlanParams* __restrict__ Pd, DevState* st,
                                                         const double* stree,
                                                         const float* srow, const float* cbox,
                                                         const float* sbox, const float* bbox,
                                                         const double* cand,
                                                         const int* cperm, const int* home, int nb,
-                                                        int* nn, double* second, double* score) {
+                                                        int* nn, double* second, double* score,
+                                                        const FleetNN* __restrict__ fnn = nullptr,
+                                                        int bp = 0) {
   const PlanParams P = *Pd;
   const int lane = lane_id();
   const long long T = st->n_nodes;
@@ -143,6 +157,7 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
   const float E32 = __double2float_ru(E * (1.0 + 1e-9));
   const float kRfac = __double2float_ru((1.0 + kNnG) * (1.0 + 3e-6));
   unsigned long long pairs = 0, tests = 0;
+  int cur = -1;  // FLEET: the plan whose counters pairs / tests hold
 #ifdef TCMP_PROF
   // clocks: [0] setup + home chunk, [1] super-chunk bounds, [2] chunk bounds, [3] chunk scans,
   // [4] final reduction
@@ -191,7 +206,12 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     const int hnl = bl ? __float_as_int(cbox[16 * (size_t)hml + 15]) : 0;
     double sl[7];
     if (bl) {
-      load7(cand + 8 * (size_t)ljl, sl);
+      if (FLEET) {
+        const int pl = ljl / bp;
+        load7(fnn[pl].cand + 8 * (size_t)(ljl - pl * bp), sl);
+      } else {
+        load7(cand + 8 * (size_t)ljl, sl);
+      }
     } else {
 #pragma unroll
       for (int k = 0; k < 7; ++k) sl[k] = 0.0;
@@ -201,6 +221,16 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     if (lane == 0) tn = atomicAdd(&st->nn_queue[qi], kNnBatch);
   for (int ib = 0; ib < jn; ++ib) {
     const int lj = __builtin_amdgcn_readlane(ljl, ib);
+    const int fpl = FLEET ? lj / bp : 0;  // plan of the candidate, its super-cells [fs0, fs1)
+    const int fs0 = FLEET ? fnn[fpl].s0 : 0, fs1 = FLEET ? fnn[fpl].s1 : nsup;
+    if (FLEET && fpl != cur) {
+      if (cur >= 0 && lane == 0) {
+        atomicAdd(&fnn[cur].st->nn_pairs, pairs);
+        atomicAdd(&fnn[cur].st->nn_box_tests, tests);
+      }
+      pairs = tests = 0;
+      cur = fpl;
+    }
     double s[7];
 #pragma unroll
     for (int k = 0; k < 7; ++k) s[k] = readlane_d(sl[k], ib);
@@ -375,12 +405,14 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     };
     if (sup_lds) {
       // super-cells from LDS, 64 per test round, zig-zagging out from the home super-cell
-      for (int gs = 0; gs < nsup; gs += 64) {
-        const int sidx = zigzag(hs, gs + lane, nsup);
+      const int nsp = fs1 - fs0;
+      for (int gs = 0; gs < nsp; gs += 64) {
+        const int zi = zigzag(hs - fs0, gs + lane, nsp);
+        const int sidx = zi >= 0 ? fs0 + zi : -1;
         int sc0 = 0, scn = 0;
         const float lbs =
             sidx >= 0 ? box_lb32<UW>(lsupf + 16 * sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
-        tests += (unsigned long long)min(64, nsup - gs);
+        tests += (unsigned long long)min(64, nsp - gs);
 #ifdef TCMP_PROF
         ++pv[0];
 #endif
@@ -396,9 +428,12 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     } else {
       // blocks of 64 super-cells, zig-zagging out from the home block (one box test each);
       // a passing block's super-cells are tested one per lane, starting at the home super
-      const int nblk = (nsup + 63) >> 6, hb = hs >> 6;
+      // (a plan's blocks: those overlapping [fs0, fs1); the blocks at its ends may hold
+      // other plans' super-cells, which the super-cell loop skips)
+      const int b0 = fs0 >> 6, nblk = ((fs1 - 1) >> 6) - b0 + 1, hb = (hs >> 6) - b0;
       for (int gb = 0; gb < nblk; gb += 64) {
-        const int bidx = zigzag(hb, gb + lane, nblk);
+        const int zb = zigzag(hb, gb + lane, nblk);
+        const int bidx = zb >= 0 ? b0 + zb : -1;
         const float lbb = bidx >= 0 ? box_lb32<UW>(bbox + 16 * (size_t)bidx, sh, sl32, w32) : INFINITY;
         tests += (unsigned long long)min(64, nblk - gb);
         uint64_t bmask = __ballot(lbb <= thr);
@@ -407,12 +442,13 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
           bmask &= bmask - 1;
           if (readlane_f(lbb, ib) > thr) continue;
           const int blk = __builtin_amdgcn_readlane(bidx, ib);
-          const int rot = blk == hb ? (hs & 63) : 0;
+          const int rot = blk == (hs >> 6) ? (hs & 63) : 0;
           const int sidx = 64 * blk + ((lane + rot) & 63);
           int sc0 = 0, scn = 0;
-          const float lbs =
-              sidx < nsup ? box_lb32<UW>(sbox + 16 * (size_t)sidx, sh, sl32, w32, &sc0, &scn) : INFINITY;
-          tests += (unsigned long long)min(64, nsup - 64 * blk);
+          const float lbs = (sidx < fs1 && sidx >= fs0)
+                                ? box_lb32<UW>(sbox + 16 * (size_t)sidx, sh, sl32, w32, &sc0, &scn)
+                                : INFINITY;
+          tests += (unsigned long long)min(64, fs1 - 64 * blk);
 #ifdef TCMP_PROF
           ++pv[0];
 #endif
@@ -439,9 +475,18 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
     const double mine = winner ? fmin(b2, lb2) : fmin(fmin(b1, b2), lb2);
     const double sec = wave_min(mine);
     if (lane == 0) {
-      nn[lj] = wi == INT_MAX ? 0 : wi;
-      if (second) second[lj] = fmin(sec, (double)thr);
-      if (score) score[lj] = m;
+      int* no = nn;
+      double *so = second, *sco = score;
+      int oi = lj;
+      if (FLEET) {
+        no = fnn[fpl].nn;
+        so = fnn[fpl].second;
+        sco = fnn[fpl].score;
+        oi = lj - fpl * bp;
+      }
+      no[oi] = wi == INT_MAX ? 0 : wi;
+      if (so) so[oi] = fmin(sec, (double)thr);
+      if (sco) sco[oi] = m;
     }
     NN_TICK(4);
   }
@@ -455,9 +500,10 @@ __global__ __launch_bounds__(kNnBlock, TCMP_NN_MINB) void k_nearest_wave32(const
       grab_slow();
     }
   }
-  if (lane == 0) {
-    atomicAdd(&st->nn_pairs, pairs);
-    atomicAdd(&st->nn_box_tests, tests);
+  if (lane == 0 && (!FLEET || cur >= 0)) {
+    DevState* const sp = FLEET ? fnn[cur].st : st;
+    atomicAdd(&sp->nn_pairs, pairs);
+    atomicAdd(&sp->nn_box_tests, tests);
 #ifdef TCMP_PROF
     for (int k = 0; k < 5; ++k) atomicAdd(&st->prof_nn[k], pc[k]);
     for (int k = 0; k < 3; ++k) atomicAdd(&st->prof_nn[5 + k], pv[k]);
