@@ -110,7 +110,7 @@ WORKLOADS = {
                     "(queries_in_flight of them planned concurrently; config_single_query = one "
                     "at a time)"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
-               queries=64, scaling="strong", pipeline=2, fleet=8,
+               queries=64, scaling="strong", pipeline=2, fleet=16,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
                     "samples each) per step, sharded round-robin over the GPUs, solved paths "
                     "gathered to rank 0 over RCCL; a GPU's queries grow their trees in fused "
@@ -330,7 +330,8 @@ def main():
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
     ap.add_argument("--fleet", type=int, default=None,
                     help="queries per fused round (tcmp_plan_run_fused) when a rank plans several "
-                         "queries per step (default 8 for c4; 0 or 1: one engine per query)")
+                         "queries per step (default 16 for c4, the best of a one-box sweep over "
+                         "4 / 8 / 16 / 31; 0 or 1: one engine per query)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
@@ -514,7 +515,22 @@ def main():
     # one-query-at-a-time throughput (config_single_query), same build, same box.
     kres = results
     single = None
-    if n_engines > 1:
+    if fleets is not None:
+        # fused rounds: S fleets one at a time on one group of engines, timed on its first
+        # engine (the fleet's kernel times are reported there; every plan counts the rounds)
+        grp = engines[:fleet]
+        grp[0].set_timing(True)
+        qs = [queries[i] for i in fleets[0]]
+        kseeds = lambda s: [step_seed(s) + 7919 * i for i in fleets[0]]  # noqa: E731
+        for w in range(max(1, args.warmup)):
+            run_fleet(grp, qs, W["samples"], W["batch"], kseeds(30_000 + 100 + w), mode, mass)
+        kres = []
+        for s in range(S):
+            kres += [r.as_dict() for r, _ in run_fleet(grp, qs, W["samples"], W["batch"],
+                                                       kseeds(30_000 + s), mode, mass)]
+        grp[0].synchronize()
+        barrier()
+    elif n_engines > 1:
         e0 = engines[0]
         e0.set_timing(True)
         obs, pack, goal = queries[0]
@@ -540,9 +556,11 @@ def main():
                   "ms_finish")}
     if args.verbose and rank == 0:
         print(json.dumps({"per_step": results, "kernel_ms_per_step": kernel_ms}), file=sys.stderr)
-    launches = sum(x["launches_nearest"] for x in kres)  # one k_edges launch per round
-    # one scan per round, except a one-node first round (nearest = the root, no index)
-    scans = sum(x["launches_nn_scan"] for x in kres)
+    # one k_edges launch per round; one scan per round, except a one-node first round (nearest =
+    # the root, no index).  The plans of a fleet share their rounds' launches.
+    launches = int(round(sum(x["launches_nearest"] / max(1, x.get("fused_plans", 0)) for x in kres)))
+    scans = int(round(sum(x["launches_nn_scan"] / max(1, x.get("fused_plans", 0)) for x in kres)))
+    ek_name = "k_fl_edges" if fleets is not None else "k_edges"
 
     # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
     # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
@@ -579,16 +597,16 @@ def main():
     ed_tf = edge_flop / (ed_ms * 1e-3) / 1e12 if ed_ms > 0 else 0.0
     peak_mixed = edge_flop / t_min / 1e12 if t_min > 0 else PEAK_FP64_TFLOPS
     roof_ed = {
-        "kernel": "k_edges", "avg_launch_ms": ed_ms / max(1, launches),
+        "kernel": ek_name, "avg_launch_ms": ed_ms / max(1, launches),
         "bound": "valu_fp64+fp32", "achieved": ed_tf, "peak": peak_mixed, "unit": "TFLOP/s",
         "frac": ed_tf / peak_mixed, "frac_fp64_contract": ed_tf / PEAK_FP64_TFLOPS,
-        "traffic": pmc_traffic("k_edges", args.workload),
+        "traffic": pmc_traffic(ek_name, args.workload),
         # the hardware's own count of the kernel's fp64 VALU flop (PMC), beside the SURVEY 8d
         # contract flop above
-        "measured_valu": pmc_valu("k_edges", args.workload, PEAK_FP64_TFLOPS),
+        "measured_valu": pmc_valu(ek_name, args.workload, PEAK_FP64_TFLOPS),
         "algorithmic": "per extend step F_fk %d + F_rne %d (fp64) + F_bp %d x %d links x %d "
                        "obstacles (packed fp32), + F_sat %d per pair past the cull (fp64); %d "
-                       "k_edges steps (rewire steps excluded), %d such pairs, %d launches" % (
+                       "edge steps (rewire steps excluded), %d such pairs, %d launches" % (
                            F_FK, f_rne, F_BP, N_LINKS, n_obs_total, F_SAT, steps, sat,
                            launches)}
     for roof, peak in ((roof_nn, PEAK_FP32_TFLOPS), (roof_ed, PEAK_FP64_TFLOPS)):
@@ -597,7 +615,7 @@ def main():
             # the PMC flop per launch over this run's event-timed average launch
             mv["tflops_live"] = mv["flop_per_launch"] / (roof["avg_launch_ms"] * 1e-3) / 1e12
             mv["frac_live"] = mv["tflops_live"] / peak
-    mv32 = pmc_valu("k_edges", args.workload, PEAK_FP32_TFLOPS, ("SQ_INSTS_VALU_FLOPS_FP32",))
+    mv32 = pmc_valu(ek_name, args.workload, PEAK_FP32_TFLOPS, ("SQ_INSTS_VALU_FLOPS_FP32",))
     mv = roof_ed["measured_valu"]
     if mv and mv32 and roof_ed["avg_launch_ms"] > 0:
         # the hardware's fp64 and fp32 flop against the same mixed bound as "frac"
@@ -650,7 +668,10 @@ def main():
                                        "+ 176 B per trajectory row, whole job"},
         "measured_peaks": measured,
         "kernel_ms_per_step": kernel_ms,
-        "kernel_timing": ("%d queries run one at a time on one engine after the timed steps "
+        "kernel_timing": ("%d fleets of %d queries run one at a time after the timed steps, "
+                          "kernel_ms per fleet (fleets in flight run untimed per kernel)" % (
+                              S, fleet) if fleets is not None else
+                          "%d queries run one at a time on one engine after the timed steps "
                           "(queries in flight run untimed per kernel)" % S
                           if kres is not results else "the timed steps"),
         # host wall time inside the C-ABI calls (rank 0; the GPU work of a step completes

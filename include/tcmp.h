@@ -231,6 +231,9 @@ typedef struct {
                              engine's lanes */
   uint64_t rewire_steps;  /* the rewire edges' extend steps (part of edge_steps, not k_edges') */
   int64_t graph_launches; /* tcmp_plan_run calls of this plan replayed as one captured graph */
+  int64_t fused_plans;    /* plans of the fused rounds this plan grew in (tcmp_plan_run_fused;
+                             0: its own rounds).  The fleet's kernel times (ms_*) are reported
+                             on its first engine, every plan counts the fleet's rounds */
   double ms_edge_prep;    /* the edge order's sort and work records before k_edges (ms_edges
                              times k_edges alone) */
 } tcmp_plan_result;

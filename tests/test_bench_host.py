@@ -134,13 +134,14 @@ def test_bench_fused_fleets(monkeypatch, capsys):
     c = line["config"]
     assert c["queries_per_step"] == 6 and c["fused_queries"] == 3
     assert c["streams_per_gpu"] == 6 and c["queries_in_flight"] == 6
-    # two fleets per step: warmup 2 steps + 2 timed steps -> 8 fused calls of 3 plans
-    assert _FakeEngine.fused == [3] * 8
+    # two fleets per step: warmup 2 steps + 2 timed steps -> 8 fused calls of 3 plans, then
+    # (1 warmup + 2) fleets one at a time for the kernel timings
+    assert _FakeEngine.fused == [3] * 11
     assert _FakeEngine.peak == 2  # two fleets in flight
-    # 4 steps x 6 queries + (1 warmup + 2) one-at-a-time kernel-timing queries, seeds distinct
-    assert len(_FakeEngine.seeds) == 27 and len(set(_FakeEngine.seeds)) == 27
+    # 4 steps x 6 queries + 3 one-at-a-time fleets x 3 queries, every seed distinct
+    assert len(_FakeEngine.seeds) == 33 and len(set(_FakeEngine.seeds)) == 33
+    assert "fleets of 3 queries" in line["kernel_timing"]
     assert line["value"] == pytest.approx(6 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)
-    assert "one at a time" in line["kernel_timing"]
 
 
 def test_bench_multi_query_pipeline(monkeypatch, capsys):

@@ -74,7 +74,7 @@ class PlanResult(ctypes.Structure):
         ("snap_sum", ctypes.c_uint64), ("nn_full_pairs", ctypes.c_uint64),
         ("launches_nn_scan", ctypes.c_int64), ("n_rewires", ctypes.c_uint64),
         ("rewire_steps", ctypes.c_uint64), ("graph_launches", ctypes.c_int64),
-        ("ms_edge_prep", ctypes.c_double),
+        ("fused_plans", ctypes.c_int64), ("ms_edge_prep", ctypes.c_double),
     ]
 
     def as_dict(self):

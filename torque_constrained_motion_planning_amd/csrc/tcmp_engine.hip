@@ -1327,6 +1327,7 @@ struct tcmp_handle {
   DBuf<long long> f_off;
   std::vector<unsigned char> f_host;
   hipEvent_t dep_ev = nullptr;
+  int fused_plans = 0;  // plans of the fused rounds the open plan grew in (0: none)
   int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
   int edge_wps = 2;    // k_edges' persistent grid, blocks per CU (environment TCMP_EDGE_WPS=1/2)
 
@@ -2863,6 +2864,7 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   h->collect_events();
   for (double& m : h->ms) m = 0;
   h->launches_nearest = 0;
+  h->fused_plans = 0;
   h->launches_scan = 0;
   h->graph_launches = 0;
   // the finish's buffers, sized here so that tcmp_plan_finish needs one host wait: waypoints
@@ -3546,6 +3548,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   r->nn_box_tests = s.nn_box_tests;
   r->ms_nn_scan = h->ms[F_NNSCAN];
   r->ms_edge_prep = h->ms[F_EDGE_PREP];
+  r->fused_plans = h->fused_plans;
   r->snap_sum = s.snap_sum;
   r->nn_full_pairs = s.nn_full_pairs;
   r->n_rewires = s.rewires;

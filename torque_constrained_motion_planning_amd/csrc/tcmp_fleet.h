@@ -408,6 +408,9 @@ int fleet_round(const Fleet& F, int nb, long long base) {
   tcmp_handle* h = F.h;
   const int K = F.K, bpb = F.bp / 256, nblk = (nb + 255) / 256;
   const dim3 pg((unsigned)(K * bpb)), b256(256);
+  // (event timing on the lead engine, when on: the fleet's kernel times are its)
+  hipEvent_t e0, e1 = nullptr;
+  h->mark_begin(F_NEAREST, &e0);
   hipLaunchKernelGGL(k_fl_sample, pg, b256, 0, h->stream, F.fp, base, nb, bpb);
   HIPCHK(hipGetLastError());
   const long long Tb = 1 + base;  // the snapshot bound: 1 + samples issued before the round
@@ -483,10 +486,14 @@ int fleet_round(const Fleet& F, int nb, long long base) {
                      h->stream, h->dP, fst, h->stree.p, h->srow.p, h->cboxf.p, h->sboxf.p,         \
                      h->bboxf.p, (const double*)nullptr, h->cperm.p, h->chome.p, nbt,             \
                      (int*)nullptr, (double*)nullptr, (double*)nullptr, F.fnn, F.bp)
+    const hipEvent_t s0 = h->mark();
     if (h->P.uniform_w) TCMP_FNNW(true); else TCMP_FNNW(false);
 #undef TCMP_FNNW
     HIPCHK(hipGetLastError());
+    e1 = h->mark_end(F_NNSCAN, s0);
   }
+  if (!e1) e1 = h->mark();
+  h->span(F_NEAREST, e0, e1);
   // edges: each plan's longest-first order (counting sort), work records, one fused k_edges
   const bool ordered = nb >= kEdgeOrderMin;
   if (ordered) {
@@ -497,18 +504,23 @@ int fleet_round(const Fleet& F, int nb, long long base) {
   }
   hipLaunchKernelGGL(k_fl_edge_records, pg, b256, 0, h->stream, F.fp, nb, ordered ? 1 : 0, bpb);
   HIPCHK(hipGetLastError());
+  const hipEvent_t ek = h->mark();
+  h->span(F_EDGE_PREP, e1, ek);
   const long long blocks = std::min<long long>(h->cu_count, ((long long)K * nb + 511) / 512);
   hipLaunchKernelGGL(k_fl_edges, dim3((unsigned)std::max<long long>(1, blocks)), dim3(512),
                      fleet_lds_bytes(F.lds_obs), h->stream, F.fp, K, nb, h->geo());
   HIPCHK(hipGetLastError());
+  const hipEvent_t ee = h->mark_end(F_EDGES, ek);
   // insertion in lane order per plan, bookkeeping, rewire
   hipLaunchKernelGGL(k_fl_ins_scan, dim3(K), dim3(1024), 0, h->stream, F.fp, nblk);
   hipLaunchKernelGGL(k_fl_ins_write, pg, b256, 0, h->stream, F.fp, nb, bpb);
   hipLaunchKernelGGL(k_fl_ins_final, dim3(1), dim3(64), 0, h->stream, F.fp, K, nb);
+  const hipEvent_t ei = h->mark_end(F_INSERT, ee);
   hipLaunchKernelGGL(k_fl_rewire_scan, pg, b256, 0, h->stream, F.fp, bpb);
   hipLaunchKernelGGL(k_fl_rewire_apply, pg, b256, stage_lds_bytes(F.max_obs), h->stream, F.fp,
                      bpb, h->geo());
   HIPCHK(hipGetLastError());
+  h->mark_end(F_REWIRE, ei);
   return 0;
 }
 
@@ -625,6 +637,7 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
     e->launches_nearest += rounds;
     e->launches_scan += scans;
     e->last_nb = last_nb;
+    e->fused_plans = n;
   }
   return 0;
 }
