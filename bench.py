@@ -207,16 +207,17 @@ def run_fleet(engs, qs, n_samples, batch, seeds, mode=_lib.TORQUE_RNE, mass=5.0,
     plan on its own engine, grow every tree in fused rounds (tcmp_plan_run_fused: one set of
     kernel launches per round for all of them), then finish and fetch each plan."""
     t0 = time.perf_counter()
-    for e, (obs, pack, goal), seed in zip(engs, qs, seeds):
+    engs = engs[:len(qs)]
+    for e, (obs, pack, goal) in zip(engs, qs):
         e.set_scene(obs, pack)
-        st = e.plan_begin(START, goal, mode, mass, exec_time, max_nodes=n_samples + 1,
-                          max_batch=batch, seed=seed)
-        if st != _lib.PLAN_OK:
-            raise RuntimeError("start/goal in collision")
+    cfgs = [_lib.plan_cfg(START, goal, mode, mass, exec_time, n_samples + 1, batch, seed)
+            for (obs, pack, goal), seed in zip(qs, seeds)]
+    if any(st != _lib.PLAN_OK for st in _lib.plan_begin_many(engs, cfgs)):
+        raise RuntimeError("start/goal in collision")
     t1 = time.perf_counter()
-    _lib.plan_run_fused(engs[:len(qs)], n_samples, batch)
+    _lib.plan_run_fused(engs, n_samples, batch)
     t2 = time.perf_counter()
-    rs = [e.plan_finish() for e in engs[:len(qs)]]
+    rs = _lib.plan_finish_many(engs)
     t3 = time.perf_counter()
     outs = [e.plan_fetch(r) if r.goal_found else None for e, r in zip(engs, rs)]
     t4 = time.perf_counter()

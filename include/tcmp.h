@@ -274,6 +274,14 @@ int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
  * (collect_data.py:74-85 plans several start/goal queries per scene step). */
 int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch);
 
+/* tcmp_plan_begin / tcmp_plan_finish on n engines (cfgs[q], results[q] for hs[q]): every
+ * engine's work is queued first, then the host waits once per engine -- a fleet's begins and
+ * finishes cost about one device round trip instead of n.  Same results as the one-engine
+ * calls; the first failing engine's error is reported (its index in the message). */
+int tcmp_plan_begin_many(tcmp_handle* const* hs, int32_t n, const tcmp_plan_cfg* cfgs,
+                         tcmp_plan_result* results);
+int tcmp_plan_finish_many(tcmp_handle* const* hs, int32_t n, tcmp_plan_result* results);
+
 /* goal node of the open plan (-1 while none) and its cost -- goal_n.cost, the bound of the
  * informed rejection test (rrt_star.py:163-165); cost may be NULL. */
 int tcmp_plan_goal(tcmp_handle* h, int64_t* node, double* cost);

@@ -89,6 +89,13 @@ def _run_bench(monkeypatch, capsys, argv):
         engines[0].plan_run(n_samples, batch)
 
     monkeypatch.setattr(_lib, "plan_run_fused", fused)
+
+    def begin_many(engines, cfgs):
+        return [e.plan_begin(None, None, 0, 0.0, 0.0, c.max_nodes, c.max_batch, c.seed)
+                for e, c in zip(engines, cfgs)]
+
+    monkeypatch.setattr(_lib, "plan_begin_many", begin_many)
+    monkeypatch.setattr(_lib, "plan_finish_many", lambda engines: [e.plan_finish() for e in engines])
     monkeypatch.setattr(sys, "argv", ["bench.py"] + argv)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
         monkeypatch.delenv(k, raising=False)

@@ -191,3 +191,34 @@ def test_c4_fleet_vs_oracle_fixture():
                 assert np.abs(out[k][sel] - f(k)).max() < 1e-9, (q, k)
     for e in es:
         e.close()
+
+
+def test_begin_finish_many_equal_single_calls():
+    """tcmp_plan_begin_many / tcmp_plan_finish_many (one host wait for a fleet's begins and
+    finishes): the same statuses, trees and results as the one-engine calls, a start-in-collision
+    plan reported by its own status among good ones."""
+    from torque_constrained_motion_planning_amd import _lib
+    plans = _plans(3, [16, 8], [2, 1], [5.0, 2.0], base=91)
+    n, batch = 8_000, 2048
+    ref = _lone(plans, [n], batch)
+    es = [_lib.Engine(0) for _ in plans]
+    cfgs = []
+    for e, q in zip(es, plans):
+        e.set_scene(q["obs"])
+        cfgs.append(_lib.plan_cfg(START, q["goal"], q["mode"], q["mass"], 5.0, n + 1, batch,
+                                  q["seed"]))
+    assert _lib.plan_begin_many(es, cfgs) == [_lib.PLAN_OK] * 3
+    for e in es:
+        e.plan_run(n, batch)
+    rs = _lib.plan_finish_many(es)
+    got = [_state(e, r, n) for e, r in zip(es, rs)]
+    assert got == ref
+    # a plan whose start collides: its own status, the others unaffected
+    bad = _lib.Engine(0)
+    box = np.array([[START[0], 0, 0.3, 1, 0, 0, 0, 1, 0, 0, 0, 1, 2.0, 2.0, 2.0]])
+    bad.set_scene(box)
+    c_bad = _lib.plan_cfg(START, plans[0]["goal"], 2, 5.0, 5.0, n + 1, batch, 1)
+    st = _lib.plan_begin_many([es[0], bad], [cfgs[0], c_bad])
+    assert st == [_lib.PLAN_OK, _lib.PLAN_START_GOAL_COLLISION]
+    for e in es + [bad]:
+        e.close()

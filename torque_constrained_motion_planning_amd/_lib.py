@@ -29,7 +29,8 @@ EXPORTS = [
     "tcmp_check_edges", "tcmp_nearest", "tcmp_minjerk", "tcmp_validate_traj",
     "tcmp_plan_begin", "tcmp_plan_round", "tcmp_plan_goal", "tcmp_plan_run", "tcmp_plan_finish",
     "tcmp_plan_retrace",
-    "tcmp_plan_run_shared", "tcmp_plan_run_group", "tcmp_plan_run_fused",
+    "tcmp_plan_run_shared", "tcmp_plan_run_group", "tcmp_plan_run_fused", "tcmp_plan_begin_many",
+    "tcmp_plan_finish_many",
     "tcmp_plan_fetch", "tcmp_plan_tree", "tcmp_plan_digest", "tcmp_plan_debug_round", "tcmp_ik", "tcmp_fk",
     "tcmp_debug_counters", "tcmp_microbench",
     "tcmp_rendezvous", "tcmp_dist_init", "tcmp_dist_destroy", "tcmp_dist_rank",
@@ -135,6 +136,10 @@ def load_library(path=LIB_PATH):
         if hasattr(L, "tcmp_plan_run_fused"):  # absent from A/B builds of older sources
             L.tcmp_plan_run_fused.argtypes = [ctypes.POINTER(vp), ctypes.c_int32, ctypes.c_int64,
                                               ctypes.c_int32]
+            L.tcmp_plan_begin_many.argtypes = [ctypes.POINTER(vp), ctypes.c_int32,
+                                               ctypes.POINTER(PlanCfg), ctypes.POINTER(PlanResult)]
+            L.tcmp_plan_finish_many.argtypes = [ctypes.POINTER(vp), ctypes.c_int32,
+                                                ctypes.POINTER(PlanResult)]
         L.tcmp_plan_finish.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_retrace.argtypes = [vp, ctypes.POINTER(PlanResult)]
         L.tcmp_plan_fetch.argtypes = [vp, _dp, _dp, _dp, _dp, _dp, _dp]
@@ -381,20 +386,8 @@ class Engine:
     def plan_begin(self, start, goal, mode, mass, exec_time, max_nodes, max_batch, seed=0,
                    weights=None, resolutions=None, radius=0.01, goal_probability=0.2,
                    goal_tolerance=1e-2):
-        cfg = PlanCfg()
-        cfg.start[:] = [float(x) for x in start]
-        cfg.goal[:] = [float(x) for x in goal]
-        cfg.weights[:] = [float(x) for x in (weights if weights is not None else [10.0] * 7)]
-        cfg.resolutions[:] = [float(x) for x in (resolutions if resolutions is not None else [0.1] * 7)]
-        cfg.radius = float(radius)
-        cfg.goal_probability = float(goal_probability)
-        cfg.goal_tolerance = float(goal_tolerance)
-        cfg.payload_mass = float(mass)
-        cfg.execution_time = float(exec_time)
-        cfg.seed = int(seed)
-        cfg.max_nodes = int(max_nodes)
-        cfg.max_batch = int(max_batch)
-        cfg.torque_mode = int(mode)
+        cfg = plan_cfg(start, goal, mode, mass, exec_time, max_nodes, max_batch, seed, weights,
+                       resolutions, radius, goal_probability, goal_tolerance)
         res = PlanResult()
         self._check(self.L.tcmp_plan_begin(self.h, ctypes.byref(cfg), ctypes.byref(res)))
         return res.status
@@ -623,6 +616,55 @@ def plan_run_group(engines, n_samples, batch):
     rc = L.tcmp_plan_run_group(arr, len(engines), int(n_samples), int(batch))
     if rc != 0:
         raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
+
+
+def plan_cfg(start, goal, mode, mass, exec_time, max_nodes, max_batch, seed=0, weights=None,
+             resolutions=None, radius=0.01, goal_probability=0.2, goal_tolerance=1e-2):
+    """tcmp_plan_cfg of one query (the reference's rrt_star arguments, rrt_star.py:151)."""
+    cfg = PlanCfg()
+    cfg.start[:] = [float(x) for x in start]
+    cfg.goal[:] = [float(x) for x in goal]
+    cfg.weights[:] = [float(x) for x in (weights if weights is not None else [10.0] * 7)]
+    cfg.resolutions[:] = [float(x) for x in (resolutions if resolutions is not None else [0.1] * 7)]
+    cfg.radius = float(radius)
+    cfg.goal_probability = float(goal_probability)
+    cfg.goal_tolerance = float(goal_tolerance)
+    cfg.payload_mass = float(mass)
+    cfg.execution_time = float(exec_time)
+    cfg.seed = int(seed)
+    cfg.max_nodes = int(max_nodes)
+    cfg.max_batch = int(max_batch)
+    cfg.torque_mode = int(mode)
+    return cfg
+
+
+def _many(engines):
+    engines = list(engines)
+    return engines, (ctypes.c_void_p * len(engines))(*[e.h.value for e in engines])
+
+
+def plan_begin_many(engines, cfgs):
+    """tcmp_plan_begin_many: plan_begin on every engine (cfgs: plan_cfg(...) each) with one
+    host wait for all of them; returns the statuses."""
+    engines, arr = _many(engines)
+    c = (PlanCfg * len(engines))(*cfgs)
+    res = (PlanResult * len(engines))()
+    L = load_library()
+    rc = L.tcmp_plan_begin_many(arr, len(engines), c, res)
+    if rc != 0:
+        raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
+    return [r.status for r in res]
+
+
+def plan_finish_many(engines):
+    """tcmp_plan_finish_many: plan_finish on every engine with one host wait for all."""
+    engines, arr = _many(engines)
+    res = (PlanResult * len(engines))()
+    L = load_library()
+    rc = L.tcmp_plan_finish_many(arr, len(engines), res)
+    if rc != 0:
+        raise TcmpError("tcmp error %d: %s" % (rc, L.tcmp_last_error().decode()))
+    return list(res)
 
 
 def plan_run_fused(engines, n_samples, batch):

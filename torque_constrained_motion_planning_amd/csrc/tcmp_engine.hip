@@ -1328,6 +1328,11 @@ struct tcmp_handle {
   std::vector<unsigned char> f_host;
   hipEvent_t dep_ev = nullptr;
   int fused_plans = 0;  // plans of the fused rounds the open plan grew in (0: none)
+  // pinned host staging of the scene's records (upload_scene: no host wait; the buffer is
+  // reused once the event of its last copy has passed)
+  void* scene_pin = nullptr;
+  size_t scene_pin_n = 0;
+  hipEvent_t scene_ev = nullptr;
   int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
   int edge_wps = 2;    // k_edges' persistent grid, blocks per CU (environment TCMP_EDGE_WPS=1/2)
 
@@ -1940,6 +1945,8 @@ int tcmp_destroy(tcmp_handle* h) {
   h->f_desc.release();
   h->f_off.release();
   if (h->dep_ev) (void)hipEventDestroy(h->dep_ev);
+  if (h->scene_ev) (void)hipEventDestroy(h->scene_ev);
+  if (h->scene_pin) (void)hipHostFree(h->scene_pin);
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
   h->cs_hist.release();
   h->cs_hoff.release();
@@ -2353,11 +2360,25 @@ int upload_scene(tcmp_handle* h) {
   }
   if (int rc = h->obs.ensure(tmp.size())) return rc;
   if (int rc = h->obs32.ensure(t32.size())) return rc;
-  HIPCHK(hipMemcpyAsync(h->obs.p, tmp.data(), tmp.size() * sizeof(double), hipMemcpyHostToDevice,
-                        h->stream));
-  HIPCHK(hipMemcpyAsync(h->obs32.p, t32.data(), t32.size() * sizeof(float), hipMemcpyHostToDevice,
-                        h->stream));
-  if (int rc_s = sync_stream(h)) return rc_s;
+  // through the handle's pinned staging: the copies are queued and the call returns (a query's
+  // set_scene no longer waits for the engine's stream); the staging is reused only after the
+  // previous scene's copies have been done
+  const size_t b64 = tmp.size() * sizeof(double), b32 = t32.size() * sizeof(float);
+  if (h->scene_ev) HIPCHK(hipEventSynchronize(h->scene_ev));
+  else HIPCHK(hipEventCreateWithFlags(&h->scene_ev, hipEventDisableTiming));
+  if (h->scene_pin_n < b64 + b32) {
+    if (h->scene_pin) HIPCHK(hipHostFree(h->scene_pin));
+    h->scene_pin = nullptr;
+    h->scene_pin_n = 0;
+    HIPCHK(hipHostMalloc(&h->scene_pin, b64 + b32));
+    h->scene_pin_n = b64 + b32;
+  }
+  unsigned char* pin = static_cast<unsigned char*>(h->scene_pin);
+  memcpy(pin, tmp.data(), b64);
+  memcpy(pin + b64, t32.data(), b32);
+  HIPCHK(hipMemcpyAsync(h->obs.p, pin, b64, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipMemcpyAsync(h->obs32.p, pin + b64, b32, hipMemcpyHostToDevice, h->stream));
+  HIPCHK(hipEventRecord(h->scene_ev, h->stream));
   h->n_obs = n;
   return 0;
 }
@@ -2810,8 +2831,13 @@ int tcmp_validate_traj(tcmp_handle* h, const double* q, const double* qd, const 
 }
 
 // ---- planner ----------------------------------------------------------------------------
-int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
-  TCMP_ENTER(h);
+}  // extern "C"
+
+namespace {
+
+// tcmp_plan_begin in two halves: everything up to the queued start / goal check and uploads,
+// then the one host wait and the status -- so that tcmp_plan_begin_many waits once for many
+int plan_begin_launch(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
   if (!cfg || !result) return fail(-1, "null cfg/result");
   if (cfg->torque_mode < 0 || cfg->torque_mode > 3) return fail(-1, "unknown torque mode");
   if (cfg->max_nodes < 2 || cfg->max_batch < 1) return fail(-1, "bad capacities");
@@ -2915,11 +2941,43 @@ int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* 
   HIPCHK(hipMemcpyAsync(h->st, &pn.st, sizeof(pn.st), hipMemcpyHostToDevice, h->stream));
   pn.P = h->P;
   HIPCHK(hipMemcpyAsync(h->dP, &pn.P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
+  return 0;
+}
+
+int plan_begin_complete(tcmp_handle* h, tcmp_plan_result* result) {
+  tcmp_handle::Pin& pn = *h->pin;
   if (int rc_s = sync_stream(h)) return rc_s;
   h->plan_open = true;
   result->n_nodes = 1;
   result->status = (pn.coll[0] || pn.coll[1]) ? TCMP_PLAN_START_GOAL_COLLISION : TCMP_PLAN_OK;
   if (result->status) h->plan_open = false;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int tcmp_plan_begin(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
+  TCMP_ENTER(h);
+  if (int rc = plan_begin_launch(h, cfg, result)) return rc;
+  return plan_begin_complete(h, result);
+}
+
+int tcmp_plan_begin_many(tcmp_handle* const* hs, int32_t n, const tcmp_plan_cfg* cfgs,
+                         tcmp_plan_result* results) {
+  Entry entry;
+  if (!hs || n < 1 || !cfgs || !results) return fail(-1, "bad arguments");
+  for (int q = 0; q < n; ++q) {
+    if (int rc = set_dev(hs[q])) return rc;
+    if (int rc = plan_begin_launch(hs[q], cfgs + q, results + q))
+      return fail(rc, "plan " + std::to_string(q) + ": " + tcmp_last_error());
+  }
+  for (int q = 0; q < n; ++q) {
+    if (int rc = set_dev(hs[q])) return rc;
+    if (int rc = plan_begin_complete(hs[q], results + q))
+      return fail(rc, "plan " + std::to_string(q) + ": " + tcmp_last_error());
+  }
   return 0;
 }
 
@@ -3465,9 +3523,19 @@ int tcmp_plan_run(tcmp_handle* h, int64_t n_samples, int32_t batch) {
   return 0;
 }
 
-// traj = false: retrace only (tcmp_plan_retrace, a foreign dynam_fn takes the waypoints)
-static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
-  TCMP_ENTER(h);
+// traj = false: retrace only (tcmp_plan_retrace, a foreign dynam_fn takes the waypoints).
+// In two halves like the begin: the finish's kernels and the state's copy, then the host wait
+// and the result (tcmp_plan_finish_many waits once for many plans).
+static void finish_launch_traj(tcmp_handle* h) {
+  hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
+  const dim3 gt(grid_for(h->kcap, 256));
+  hipLaunchKernelGGL(TCMP_BY_MODE(k_traj, h->P.torque_mode), gt, dim3(256), 0, h->stream, h->dP,
+                     h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p, h->kcap);
+  hipLaunchKernelGGL(k_traj_tau, gt, dim3(256), 0, h->stream, h->st, h->tq.p, h->tqd.p,
+                     h->tqdd.p, h->ttau.p, h->kcap);
+  hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
+}
+static int plan_finish_launch(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   if (!r) return fail(-1, "null result");
   if (!h->plan_open) return fail(-1, "no open plan");
   memset(r, 0, sizeof(*r));
@@ -3479,20 +3547,14 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   hipLaunchKernelGGL(k_retrace, dim3(1), dim3(256), 0, h->stream, h->dP, h->st,
                      Tree{h->cfg.p, h->parent.p, h->tgt.p, h->meta.p}, h->chain.p, h->wp.p,
                      (long long)(h->wp.n / 7));
-  auto launch_traj = [&]() {
-    hipLaunchKernelGGL(k_traj_prep, dim3(1), dim3(1), 0, h->stream, h->st);
-    const dim3 gt(grid_for(h->kcap, 256));
-    hipLaunchKernelGGL(TCMP_BY_MODE(k_traj, h->P.torque_mode), gt, dim3(256), 0, h->stream, h->dP,
-                       h->st, h->wp.p, h->tq.p, h->tqd.p, h->tqdd.p, h->tpsg.p, h->kcap);
-    hipLaunchKernelGGL(k_traj_tau, gt, dim3(256), 0, h->stream, h->st, h->tq.p, h->tqd.p,
-                       h->tqdd.p, h->ttau.p, h->kcap);
-    hipLaunchKernelGGL(k_traj_post, dim3(1), dim3(1), 0, h->stream, h->st);
-  };
-  if (traj) launch_traj();
+  if (traj) finish_launch_traj(h);
   HIPCHK(hipGetLastError());
   h->mark_end(F_FINISH, e0);
+  HIPCHK(hipMemcpyAsync(&h->pin->st, h->st, sizeof(DevState), hipMemcpyDeviceToHost, h->stream));
+  return 0;
+}
+static int plan_finish_complete(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   DevState& s = h->pin->st;
-  HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   if (int rc_s = sync_stream(h)) return rc_s;
   r->goal_node = s.goal_node;
   if (s.overflow == 1) return fail(-3, "tree capacity exceeded");
@@ -3515,7 +3577,7 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
       rc = rc ? rc : h->ttau.ensure(K * 7);
       if (rc) return rc;
       h->kcap = K;
-      launch_traj();
+      finish_launch_traj(h);
       HIPCHK(hipGetLastError());
       HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
       if (int rc_s = sync_stream(h)) return rc_s;
@@ -3557,9 +3619,31 @@ static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
   return 0;
 }
 
+static int plan_finish_impl(tcmp_handle* h, tcmp_plan_result* r, bool traj) {
+  TCMP_ENTER(h);
+  if (int rc = plan_finish_launch(h, r, traj)) return rc;
+  return plan_finish_complete(h, r, traj);
+}
+
 int tcmp_plan_finish(tcmp_handle* h, tcmp_plan_result* r) { return plan_finish_impl(h, r, true); }
 
 int tcmp_plan_retrace(tcmp_handle* h, tcmp_plan_result* r) { return plan_finish_impl(h, r, false); }
+
+int tcmp_plan_finish_many(tcmp_handle* const* hs, int32_t n, tcmp_plan_result* results) {
+  Entry entry;
+  if (!hs || n < 1 || !results) return fail(-1, "bad arguments");
+  for (int q = 0; q < n; ++q) {
+    if (int rc = set_dev(hs[q])) return rc;
+    if (int rc = plan_finish_launch(hs[q], results + q, true))
+      return fail(rc, "plan " + std::to_string(q) + ": " + tcmp_last_error());
+  }
+  for (int q = 0; q < n; ++q) {
+    if (int rc = set_dev(hs[q])) return rc;
+    if (int rc = plan_finish_complete(hs[q], results + q, true))
+      return fail(rc, "plan " + std::to_string(q) + ": " + tcmp_last_error());
+  }
+  return 0;
+}
 
 int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, double* qdd,
                     double* psg, double* tau) {
