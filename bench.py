@@ -110,7 +110,7 @@ WORKLOADS = {
                     "(queries_in_flight of them planned concurrently; config_single_query = one "
                     "at a time)"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
-               queries=64, scaling="strong", pipeline=2, fleet=16,
+               queries=64, scaling="strong", pipeline=3, fleet=16,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
                     "samples each) per step, sharded round-robin over the GPUs, solved paths "
                     "gathered to rank 0 over RCCL; a GPU's queries grow their trees in fused "
@@ -337,8 +337,8 @@ def main():
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
                          "kernel tails overlap another's kernels (not with --shared-tree); "
-                         "default per workload (c2 8, c3 4, c4 2, c5 2: the best of a one-box "
-                         "sweep); --pipeline 1 runs the steps one after another")
+                         "default per workload (c2 8, c3 4, c4 3 fleets, c5 2: the best of a "
+                         "one-box sweep); --pipeline 1 runs the steps one after another")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
