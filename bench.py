@@ -405,15 +405,18 @@ def main():
     # with --pipeline P run P consecutive steps at once the same way (step s on engine s mod P).
     pipe = max(1, args.pipeline if args.pipeline is not None else W.get("pipeline", 1)) \
         if not shared else 1
+    # fused rounds (tcmp_plan_run_fused): the (query, step) pairs of the steps in flight, in
+    # order, are dealt in fleets of `fleet` -- c4: a step's queries; a single-query workload:
+    # consecutive steps' queries (each its own seed) -- with `pipe` fleets in flight, each on
+    # its own group of engines
     fleet = args.fleet if args.fleet is not None else W.get("fleet", 0)
-    fleet = min(fleet, len(queries)) if len(queries) > 1 and not shared else 0
-    if fleet > 1:
-        # fleets of `fleet` queries, `pipe` of them in flight (a group of engines each)
-        fleets = [list(range(f, min(f + fleet, len(queries)))) for f in range(0, len(queries), fleet)]
-        n_streams = max(1, min(len(fleets) * pipe, args.streams if args.streams else pipe))
+    fleet = 0 if shared or W["meshes"] or args.self_collisions else fleet
+    fleets = fleet > 1
+    if fleets:
+        n_streams = max(1, args.streams if args.streams else pipe)
         n_engines = n_streams * fleet
     else:
-        fleets = None
+        fleet = 0
         n_streams = max(1, min(len(queries) * pipe, args.streams if args.streams else 16))
         n_engines = n_streams
     engines = [eng] + [_lib.Engine(gpu) for _ in range(n_engines - 1)]
@@ -432,9 +435,10 @@ def main():
             e.set_timing(False)
 
     def run_jobs(jobs):
-        """jobs: (query index, step) pairs.  Each engine's thread takes the next job as soon as
-        its last one is done, so P steps stay in flight the whole time (no barrier between
-        groups of steps, no idle GPU while the slowest query of a group finishes)."""
+        """jobs: (query index, step) pairs, or lists of them (fleets).  Each engine's thread
+        takes the next job as soon as its last one is done, so P steps stay in flight the whole
+        time (no barrier between groups of steps, no idle GPU while the slowest query of a
+        group finishes)."""
         nxt = iter(range(len(jobs)))
         take = threading.Lock()
 
@@ -445,15 +449,15 @@ def main():
                     idx = next(nxt, None)
                 if idx is None:
                     return got
-                j, s = jobs[idx]
-                if fleets is not None:
-                    # job j = fleet j of step s on this thread's group of engines
-                    qs = fleets[j]
-                    done = run_fleet(engines[k * fleet:(k + 1) * fleet], [queries[i] for i in qs],
-                                     W["samples"], W["batch"],
-                                     [step_seed(s) + 7919 * i for i in qs], mode, mass)
-                    got += [(idx * fleet + t, s) + d for t, d in enumerate(done)]
+                if fleets:
+                    # a fleet of (query, step) pairs on this thread's group of engines
+                    pairs = jobs[idx]
+                    done = run_fleet(engines[k * fleet:(k + 1) * fleet],
+                                     [queries[j] for j, _ in pairs], W["samples"], W["batch"],
+                                     [step_seed(s) + 7919 * j for j, s in pairs], mode, mass)
+                    got += [(idx * fleet + t, s) + d for t, ((_, s), d) in enumerate(zip(pairs, done))]
                     continue
+                j, s = jobs[idx]
                 obs, pack, goal = queries[j]
                 got.append((idx, s) + run_query(engines[k], obs, goal, W["samples"], W["batch"],
                                                 step_seed(s) + 7919 * j, mode, mass, meshes=pack,
@@ -462,8 +466,9 @@ def main():
                       key=lambda x: x[0])
 
     def step_group(ss):
-        done = run_jobs([(j, s) for s in ss
-                         for j in range(len(fleets) if fleets is not None else len(queries))])
+        pairs = [(j, s) for s in ss for j in range(len(queries))]
+        done = run_jobs([pairs[i:i + fleet] for i in range(0, len(pairs), fleet)] if fleets
+                        else pairs)
         res = []
         for s in ss:
             part = [d for d in done if d[1] == s]
@@ -486,7 +491,8 @@ def main():
 
     log("workload %s ready on rank %d of %d" % (args.workload, rank, world))
     if args.warmup:
-        step_group([10_000 + i for i in range(args.warmup * pipe)])
+        step_group([10_000 + i for i in range(
+            args.warmup * pipe * (fleet if fleets and len(queries) == 1 else 1))])
     log("warmup done")
 
     barrier()
@@ -516,13 +522,15 @@ def main():
     # one-query-at-a-time throughput (config_single_query), same build, same box.
     kres = results
     single = None
-    if fleets is not None:
+    if fleets:
         # fused rounds: S fleets one at a time on one group of engines, timed on its first
-        # engine (the fleet's kernel times are reported there; every plan counts the rounds)
+        # engine (the fleet's kernel times are reported there; every plan counts the rounds);
+        # a fleet = the first `fleet` (query, step) pairs' queries, fresh seeds
         grp = engines[:fleet]
         grp[0].set_timing(True)
-        qs = [queries[i] for i in fleets[0]]
-        kseeds = lambda s: [step_seed(s) + 7919 * i for i in fleets[0]]  # noqa: E731
+        ids = [t % len(queries) for t in range(fleet)]
+        qs = [queries[j] for j in ids]
+        kseeds = lambda s: [step_seed(s) + 7919 * t for t in range(fleet)]  # noqa: E731
         for w in range(max(1, args.warmup)):
             run_fleet(grp, qs, W["samples"], W["batch"], kseeds(30_000 + 100 + w), mode, mass)
         kres = []
@@ -530,8 +538,9 @@ def main():
             kres += [r.as_dict() for r, _ in run_fleet(grp, qs, W["samples"], W["batch"],
                                                        kseeds(30_000 + s), mode, mass)]
         grp[0].synchronize()
+        grp[0].set_timing(False)
         barrier()
-    elif n_engines > 1:
+    if n_engines > 1 and (not fleets or len(queries) == 1):
         e0 = engines[0]
         e0.set_timing(True)
         obs, pack, goal = queries[0]
@@ -540,17 +549,19 @@ def main():
                       mass, meshes=pack)
         e0.synchronize()
         t1 = time.perf_counter()
-        kres = [run_query(e0, obs, goal, W["samples"], W["batch"], step_seed(30_000 + s), mode,
-                          mass, meshes=pack)[0].as_dict() for s in range(S)]
+        kq = [run_query(e0, obs, goal, W["samples"], W["batch"], step_seed(30_000 + s), mode,
+                        mass, meshes=pack)[0].as_dict() for s in range(S)]
         e0.synchronize()
         dts = time.perf_counter() - t1
+        if not fleets:
+            kres = kq
         if len(queries) == 1:
-            single = {"value": sum(x["n_samples"] for x in kres) / dts * world,
+            single = {"value": sum(x["n_samples"] for x in kq) / dts * world,
                       "unit": "samples/s", "ms_per_step": dts / S * 1e3, "steps": S,
                       "queries_in_flight": 1,
                       "note": "the same workload one query at a time on one engine per GPU, "
                               "after the timed region (rank 0's time x ranks); the headline "
-                              "value keeps %d queries in flight" % pipe}
+                              "value keeps %d queries in flight" % (pipe * max(1, fleet))}
         barrier()
     kernel_ms = {k: sum(x[k] for x in kres) / S for k in
                  ("ms_nearest", "ms_nn_scan", "ms_edge_prep", "ms_edges", "ms_insert", "ms_rewire",
@@ -561,7 +572,7 @@ def main():
     # the root, no index).  The plans of a fleet share their rounds' launches.
     launches = int(round(sum(x["launches_nearest"] / max(1, x.get("fused_plans", 0)) for x in kres)))
     scans = int(round(sum(x["launches_nn_scan"] / max(1, x.get("fused_plans", 0)) for x in kres)))
-    ek_name = "k_fl_edges" if fleets is not None else "k_edges"
+    ek_name = "k_fl_edges" if fleets else "k_edges"
 
     # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
     # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
@@ -656,7 +667,7 @@ def main():
                    "batch_per_round": W["batch"], "execution_time_s": 5.0,
                    "parallelism": ("shared-tree x%d" if shared else "query-sharded x%d") % world,
                    "streams_per_gpu": n_engines, "pipelined_steps": pipe,
-                   "queries_in_flight": (min(n_streams * fleet, len(queries) * pipe) if fleets
+                   "queries_in_flight": (n_streams * fleet if fleets
                                          else min(n_streams, len(queries) * pipe)),
                    "fused_queries": fleet if fleets else 1,
                    "self_collisions": bool(args.self_collisions)},
@@ -671,7 +682,7 @@ def main():
         "kernel_ms_per_step": kernel_ms,
         "kernel_timing": ("%d fleets of %d queries run one at a time after the timed steps, "
                           "kernel_ms per fleet (fleets in flight run untimed per kernel)" % (
-                              S, fleet) if fleets is not None else
+                              S, fleet) if fleets else
                           "%d queries run one at a time on one engine after the timed steps "
                           "(queries in flight run untimed per kernel)" % S
                           if kres is not results else "the timed steps"),
