@@ -99,12 +99,12 @@ def pmc_valu(kernel, workload, peak, counters=("SQ_INSTS_VALU_FLOPS_FP64",)):
 # 32,768), 262,144 for the 1e6 / 1e7-sample ones.
 WORKLOADS = {
     "c2": dict(boxes=4, meshes=0, mode=_lib.TORQUE_NOV, mass=2.0, samples=100_000, batch=65536,
-               queries=1, scaling="weak", pipeline=8,
+               queries=1, scaling="weak", pipeline=3, fleet=8,
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step (queries_in_flight "
                     "of them planned concurrently)"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
-               batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=4,
+               batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=2, fleet=4,
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step "
                     "(queries_in_flight of them planned concurrently; config_single_query = one "
@@ -330,15 +330,17 @@ def main():
                     help="engines (one HIP stream each) driven concurrently by host threads "
                          "when a rank plans several queries per step (default 16 for c4, at most one per query)")
     ap.add_argument("--fleet", type=int, default=None,
-                    help="queries per fused round (tcmp_plan_run_fused) when a rank plans several "
-                         "queries per step (default 16 for c4, the best of a one-box sweep over "
-                         "4 / 8 / 16 / 31; 0 or 1: one engine per query)")
+                    help="queries per fused round (tcmp_plan_run_fused): a step's queries (c4) or "
+                         "consecutive steps' queries (c2, c3) grow their trees in one set of "
+                         "launches per round (default c2 8, c3 4, c4 16, the best of a one-box "
+                         "sweep; 0 or 1: one engine per query; box scenes only)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
                          "kernel tails overlap another's kernels (not with --shared-tree); "
-                         "default per workload (c2 8, c3 4, c4 3 fleets, c5 2: the best of a "
-                         "one-box sweep); --pipeline 1 runs the steps one after another")
+                         "default per workload (c2 3 fleets of 8, c3 2 fleets of 4, c4 3 fleets "
+                         "of 16, c5 2 queries: the best of a one-box sweep); --pipeline 1 --fleet "
+                         "0 runs the steps one after another")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -532,11 +534,11 @@ def main():
         qs = [queries[j] for j in ids]
         kseeds = lambda s: [step_seed(s) + 7919 * t for t in range(fleet)]  # noqa: E731
         for w in range(max(1, args.warmup)):
-            run_fleet(grp, qs, W["samples"], W["batch"], kseeds(30_000 + 100 + w), mode, mass)
+            run_fleet(grp, qs, W["samples"], W["batch"], kseeds(40_000 + 100 + w), mode, mass)
         kres = []
         for s in range(S):
             kres += [r.as_dict() for r, _ in run_fleet(grp, qs, W["samples"], W["batch"],
-                                                       kseeds(30_000 + s), mode, mass)]
+                                                       kseeds(40_000 + s), mode, mass)]
         grp[0].synchronize()
         grp[0].set_timing(False)
         barrier()

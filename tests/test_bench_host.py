@@ -108,8 +108,8 @@ def _run_bench(monkeypatch, capsys, argv):
 @pytest.mark.parametrize("pipe", [1, 2])
 def test_bench_pipelined_single_query_steps(monkeypatch, capsys, pipe):
     line = _run_bench(monkeypatch, capsys, ["--workload", "c2", "--steps", "4", "--warmup", "1",
-                                            "--pipeline", str(pipe), "--no-cpu-baseline",
-                                            "--no-alt"])
+                                            "--pipeline", str(pipe), "--fleet", "0",
+                                            "--no-cpu-baseline", "--no-alt"])
     assert line["steps"] == 4 and line["value"] > 0
     assert line["config"]["pipelined_steps"] == pipe
     assert line["config"]["streams_per_gpu"] == pipe
@@ -149,6 +149,24 @@ def test_bench_fused_fleets(monkeypatch, capsys):
     assert len(_FakeEngine.seeds) == 33 and len(set(_FakeEngine.seeds)) == 33
     assert "fleets of 3 queries" in line["kernel_timing"]
     assert line["value"] == pytest.approx(6 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)
+
+
+def test_bench_single_query_fleets(monkeypatch, capsys):
+    """c3's default: consecutive steps' queries (one per step, each its own seed) in fleets of
+    `fleet`, `pipeline` fleets in flight; the one-query-at-a-time line rides beside it."""
+    line = _run_bench(monkeypatch, capsys, ["--workload", "c3", "--steps", "6", "--warmup", "1",
+                                            "--fleet", "4", "--pipeline", "2",
+                                            "--no-cpu-baseline", "--no-alt"])
+    c = line["config"]
+    assert c["fused_queries"] == 4 and c["queries_in_flight"] == 8 and c["streams_per_gpu"] == 8
+    # warmup 1 x 2 x 4 = 8 steps (2 fleets), timed 6 steps (4 + 2), 1 + 6 kernel-timing fleets
+    assert sorted(_FakeEngine.fused) == [2] + [4] * 10  # (two threads: any order)
+    assert line["steps"] == 6 and line["value"] > 0
+    sq = line["config_single_query"]
+    assert sq["queries_in_flight"] == 1 and sq["steps"] == 6
+    # 8 + 6 + 7 x 4 fleet queries, + (1 + 6) one at a time: every seed distinct
+    n = 8 + 6 + 28 + 7
+    assert len(_FakeEngine.seeds) == n and len(set(_FakeEngine.seeds)) == n
 
 
 def test_bench_multi_query_pipeline(monkeypatch, capsys):
