@@ -251,8 +251,8 @@ __global__ __launch_bounds__(256) void k_fl_edge_records(const FleetPlan* __rest
 // k_edges over every plan's edges (box scenes, one lane per edge): the same persistent walk and
 // the same per-step tests (rrt_star.py:90-98), with each wave bound to one plan at a time.  A
 // wave starts at plan (its index * K / waves); when that plan's queue is empty and its lanes
-// have finished, it posts its counts to the plan and takes the next plan, until it has found
-// every plan's queue empty.  n: the round's edge count (every plan's).
+// have finished, it posts its counts to the plan and takes the next plan, until it has been
+// through all K.  nb: the round's edge count (every plan's).
 __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict__ fp, int K, int nb,
                                                      Geo g_g) {
   extern __shared__ double tcmp_lds[];
@@ -264,11 +264,14 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
   const int lane = lane_id();
   const int waves = gridDim.x * (blockDim.x >> 6);
   int plan = (int)((long long)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * K / waves);
-  // the plan's fields are read through F where they are used (scalar loads), so that nothing of
-  // the plan stays live in registers across the collision check
-  const FleetPlan* F = fp + plan;
-  int idle = 0;       // plans in a row in which the wave found no edge
-  bool got = false;   // the wave took an edge of its current plan
+  // the plan's fields are read through F where they are used: scalar loads from the constant
+  // address space, which the compiler may repeat instead of keeping the values live in
+  // registers across the collision check
+  typedef const __attribute__((address_space(4))) FleetPlan CFleetPlan;
+  CFleetPlan* const fc = (CFleetPlan*)(uintptr_t)fp;
+  CFleetPlan* F = fc + plan;
+  // a plan's queue never refills once empty, so each wave visits each plan once
+  int visited = 1;
   int e = -1, i = 0, n = 0;
   bool done = false;
   double q[7];
@@ -299,7 +302,6 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
           done = true;
         }
       }
-      got = got || __ballot(e >= 0);
     }
     if (__ballot(!done) == 0) {
       // this plan's queue is empty and its lanes are done: its counts, then the next plan
@@ -312,11 +314,9 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
       }
       steps = 0;
       ss = StepStats{};
-      idle = got ? 0 : idle + 1;
-      if (idle >= K) break;
-      got = false;
+      if (visited++ == K) break;
       plan = plan + 1 == K ? 0 : plan + 1;
-      F = fp + plan;
+      F = fc + plan;
       done = false;
       continue;
     }
