@@ -575,6 +575,8 @@ def main():
     launches = int(round(sum(x["launches_nearest"] / max(1, x.get("fused_plans", 0)) for x in kres)))
     scans = int(round(sum(x["launches_nn_scan"] / max(1, x.get("fused_plans", 0)) for x in kres)))
     ek_name = "k_fl_edges" if fleets else "k_edges"
+    # (the fused-rounds scan's PMC entry: tools/pmc_summary.py)
+    nn_key = "k_nearest_wave32@fleet" if fleets else "k_nearest_wave32"
 
     # k_nearest_wave32: 21 flop (fp32 first pass) per (candidate, node) pair it evaluated.  The
     # brute-force-equivalent rate (SURVEY 8d F_nn = 21 T per sample) counts pairs the pruned
@@ -584,10 +586,11 @@ def main():
     nn_ms = sum(x["ms_nn_scan"] for x in kres)
     nn_tf = NN_FLOP_PER_PAIR * nn_pairs / (nn_ms * 1e-3) / 1e12 if nn_ms > 0 else 0.0
     roof_nn = {
-        "kernel": "k_nearest_wave32", "avg_launch_ms": nn_ms / max(1, scans),
+        "kernel": "k_nearest_wave32<FLEET>" if fleets else "k_nearest_wave32",
+        "avg_launch_ms": nn_ms / max(1, scans),
         "bound": "valu_fp32", "achieved": nn_tf, "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-        "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic("k_nearest_wave32", args.workload),
-        "measured_valu": pmc_valu("k_nearest_wave32", args.workload, PEAK_FP32_TFLOPS,
+        "frac": nn_tf / PEAK_FP32_TFLOPS, "traffic": pmc_traffic(nn_key, args.workload),
+        "measured_valu": pmc_valu(nn_key, args.workload, PEAK_FP32_TFLOPS,
                                   ("SQ_INSTS_VALU_FLOPS_FP32",)),
         "algorithmic": "%d flop per evaluated (candidate, node) pair; %d pairs over %d launches "
                        "(brute force would be %d pairs: %.1f PFLOP/s equivalent)" % (

@@ -22,6 +22,13 @@ set -e -o pipefail
 TAG=${1:?tag}; shift
 O=gpurun_out/$TAG; mkdir -p $O
 export TMPDIR=/tmp
+pmc_args() {  # workload -> bench.py arguments of a counter pass: whole fleets, one in flight
+  case "$1" in
+    c3|"") echo "--steps 4 --warmup 0 --pipeline 1" ;;   # one fleet of 4 (+ the timing pass's)
+    c2) echo "--workload c2 --steps 8 --warmup 0 --pipeline 1" ;;
+    *) echo "--workload $1 --steps 1 --warmup 0 --pipeline 1" ;;
+  esac
+}
 bench_args() {  # workload -> bench.py arguments of one measured line
   case "$1" in
     c5) echo "--workload c5 --steps 2 --warmup 1" ;;
@@ -54,27 +61,23 @@ for st in "$@"; do
       for grp in FETCH_SIZE WRITE_SIZE; do
         i=$((i+1))
         timeout -s KILL 300 rocprofv3 --pmc $grp --kernel-trace -d $O/pmc_$w/p$i -o run --output-format csv \
-          -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-          --pipeline 1 --no-cpu-baseline --no-alt > $O/pmc_${w}_p$i.log 2>&1
+          -- python3 bench.py $(pmc_args $w) --no-cpu-baseline --no-alt > $O/pmc_${w}_p$i.log 2>&1
       done ;;
     sq)
       w=${arg:-c3}
       timeout -s KILL 300 rocprofv3 --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU \
         --kernel-trace -d $O/sq_$w -o run --output-format csv \
-        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-        --pipeline 1 --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
+        -- python3 bench.py $(pmc_args $w) --no-cpu-baseline --no-alt > $O/sq_$w.log 2>&1 ;;
     valu)
       w=${arg:-c3}
       timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS_LDS SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_FMA_F32 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_TRANS_F64 SQ_INSTS_VALU_FLOPS_FP32 SQ_INSTS_VALU_FLOPS_FP64 \
         --kernel-trace -d $O/valu_$w -o run --output-format csv \
-        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-        --pipeline 1 --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
+        -- python3 bench.py $(pmc_args $w) --no-cpu-baseline --no-alt > $O/valu_$w.log 2>&1 ;;
     mix)
       w=${arg:-c3}
       timeout -s KILL 300 rocprofv3 --pmc SQ_INSTS SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_BRANCH SQ_INSTS_LDS SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_THREAD_CYCLES_VALU \
         --kernel-trace -d $O/mix_$w -o run --output-format csv \
-        -- python3 bench.py $(bench_args $w | sed 's/--steps [0-9]*/--steps 1/; s/--warmup [0-9]*/--warmup 0/') \
-        --pipeline 1 --no-cpu-baseline --no-alt > $O/mix_$w.log 2>&1 ;;
+        -- python3 bench.py $(pmc_args $w) --no-cpu-baseline --no-alt > $O/mix_$w.log 2>&1 ;;
     prof)
       P=torque_constrained_motion_planning_amd/libtcmp_prof.so
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err

@@ -5,7 +5,8 @@ Usage: python tools/pmc_summary.py OUT.json NOTE PASS_DIR [PASS_DIR ...]
 Each PASS_DIR is one `rocprofv3 --pmc <COUNTER> --kernel-trace -d PASS_DIR -o run
 --output-format csv -- python3 bench.py ...` run (one TCC counter per pass: FETCH_SIZE and
 WRITE_SIZE do not fit one pass on gfx950).  Kernel names are reduced to the bare function name
-(template arguments and parameters stripped).  Values are per dispatch, in KiB as rocprofv3
+(template arguments and parameters stripped; the fleet scan k_nearest_wave32<.., true> is
+`k_nearest_wave32@fleet`).  Values are per dispatch, in KiB as rocprofv3
 reports them; bench.py applies the gfx950 correction (x2 on FETCH_SIZE) when it reads them.
 """
 import csv
@@ -17,6 +18,14 @@ import sys
 
 
 def short(name):
+    # the fused-rounds instantiation of the scan (k_nearest_wave32<UW, SW, true>) is its own
+    # entry: its launches serve a whole fleet
+    fleet = re.search(r"k_nearest_wave32<[^>]*, true>", name) is not None
+    name = short_base(name)
+    return name + "@fleet" if fleet else name
+
+
+def short_base(name):
     name = name.replace("(anonymous namespace)::", "")
     name = re.sub(r"\(.*$", "", name)
     name = re.sub(r"<.*$", "", name)

@@ -5,16 +5,22 @@ launch) and those that ran alone (bench.py's one-at-a-time kernel-timing pass), 
 line's event-timed `avg_launch_ms` can be checked against the trace of the same command.
 Launches of a few hundred threads (the bench's scene setup) are left out, as in bench.py.
 
-usage: python tools/trace_split.py RUN_kernel_trace.csv [kernel-substring ...]
+usage: python tools/trace_split.py RUN_kernel_trace.csv [kernel ...]
+Kernels are named as tools/pmc_summary.py names them (the fused-rounds scan is
+`k_nearest_wave32@fleet`).
 """
 import csv
 import json
+import os
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from pmc_summary import short  # noqa: E402
 
 
 def main():
     path = sys.argv[1]
-    want = sys.argv[2:] or ["k_edges", "k_nearest_wave32"]
+    want = sys.argv[2:] or ["k_edges", "k_fl_edges", "k_nearest_wave32", "k_nearest_wave32@fleet"]
     rows = list(csv.DictReader(open(path)))
     # every dispatch as (start, end, queue): a launch "overlapped" if any dispatch of another
     # queue (another engine's stream) ran during it
@@ -28,7 +34,7 @@ def main():
 
     out = {}
     for k in want:
-        ks = [r for r in rows if k in r["Kernel_Name"]]
+        ks = [r for r in rows if short(r["Kernel_Name"]) == k]
         if not ks:
             continue
         big = max(int(r["Grid_Size_X"]) for r in ks)
