@@ -95,7 +95,9 @@ __device__ __forceinline__ float box_lb32(const float* b, const float sh[7], con
 #define TCMP_NN_MINB 1  // min blocks per CU the register allocation must allow
 #endif
 // The scan's workgroups are 1024 threads (16 waves, one workgroup per CU at 4 waves per SIMD)
-// and hold the super-cell boxes in LDS when there are at most kNnLdsSup of them (64 KB): the
+// and hold the super-cell boxes in LDS when there are at most kNnLdsSup of them (128 KB, which
+// costs no occupancy: the VGPRs already allow one workgroup per CU; a fused round's index over
+// four 1e6-sample plans has ~1,600 super-cells -- 4.65 -> 4.31 ms per C3 fleet scan): the
 // super-cell tests then cost an LDS round trip instead of an L2 one, and the block level (whose
 // only job is to save super-cell box loads) is skipped.  Larger indexes walk the blocks from
 // global memory as before.  (One walk over a flat pointer serving both was 5 % slower.)
@@ -104,7 +106,7 @@ __device__ __forceinline__ float box_lb32(const float* b, const float sh[7], con
 #endif
 constexpr int kNnBlock = TCMP_NN_BLOCK;
 #ifndef TCMP_NN_LDS_SUP
-#define TCMP_NN_LDS_SUP 1024
+#define TCMP_NN_LDS_SUP 2048
 #endif
 constexpr int kNnLdsSup = TCMP_NN_LDS_SUP;
 // SW: cells per scan round (2 in the engine).  Passing cells queue up across super-cells (the queue
