@@ -446,7 +446,7 @@ class Engine:
         out = np.zeros(4)
         self._check(self.L.tcmp_microbench(self.h, _d(out)))
         return {"fp64_tflops": float(out[0]), "fp32_tflops": float(out[1]),
-                "hbm_gbs": float(out[2])}
+                "hbm_gbs": float(out[2]), "hbm_copy_variant": int(out[3])}
 
     def plan_digest(self):
         """(digest, n_nodes) of the open plan's tree, computed on the device (tcmp_plan_digest;
