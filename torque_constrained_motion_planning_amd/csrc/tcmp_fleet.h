@@ -589,6 +589,8 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
   // the fleet index lives in the lead engine's index buffers (its own plan uses none of them
   // during a fused round), sized for every plan's nodes and lanes
   const long long Tmax = 1 + h->samples_issued + n_samples;
+  if ((long long)n * Tmax >= INT_MAX || (long long)n * F.bp >= INT_MAX)
+    return fail(-1, "a fleet's node or lane slots exceed 2^31 (fewer plans per fleet)");
   if (int rc = ensure_index(h, (size_t)n * (size_t)Tmax, (size_t)n * (size_t)F.bp)) return rc;
   if (int rc = h->chome.ensure(2 * (size_t)n * (size_t)F.bp)) return rc;
   if (int rc = h->f_off.ensure((size_t)n + 1)) return rc;
