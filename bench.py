@@ -457,7 +457,7 @@ def main():
                     done = run_fleet(engines[k * fleet:(k + 1) * fleet],
                                      [queries[j] for j, _ in pairs], W["samples"], W["batch"],
                                      [step_seed(s) + 7919 * j for j, s in pairs], mode, mass)
-                    got += [(idx * fleet + t, s) + d for t, ((_, s), d) in enumerate(zip(pairs, done))]
+                    got += [(idx * fleet + t, s) + d for t, ((_, s), d) in enumerate(zip(pairs, done))]  # noqa: E501
                     continue
                 j, s = jobs[idx]
                 obs, pack, goal = queries[j]
@@ -469,7 +469,10 @@ def main():
 
     def step_group(ss):
         pairs = [(j, s) for s in ss for j in range(len(queries))]
-        done = run_jobs([pairs[i:i + fleet] for i in range(0, len(pairs), fleet)] if fleets
+        # (fleets of at most `fleet`, and no larger than it takes to keep every thread's group
+        # busy: a few steps dealt as one fleet would leave the other groups idle)
+        size = max(1, min(fleet, -(-len(pairs) // n_streams))) if fleets else 1
+        done = run_jobs([pairs[i:i + size] for i in range(0, len(pairs), size)] if fleets
                         else pairs)
         res = []
         for s in ss:

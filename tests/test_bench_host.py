@@ -159,8 +159,9 @@ def test_bench_single_query_fleets(monkeypatch, capsys):
                                             "--no-cpu-baseline", "--no-alt"])
     c = line["config"]
     assert c["fused_queries"] == 4 and c["queries_in_flight"] == 8 and c["streams_per_gpu"] == 8
-    # warmup 1 x 2 x 4 = 8 steps (2 fleets), timed 6 steps (4 + 2), 1 + 6 kernel-timing fleets
-    assert sorted(_FakeEngine.fused) == [2] + [4] * 10  # (two threads: any order)
+    # warmup 1 x 2 x 4 = 8 steps (2 fleets of 4), timed 6 steps (two fleets of 3: one per
+    # thread, rather than 4 + 2), 1 + 6 kernel-timing fleets of 4
+    assert sorted(_FakeEngine.fused) == [3, 3] + [4] * 9  # (two threads: any order)
     assert line["steps"] == 6 and line["value"] > 0
     sq = line["config_single_query"]
     assert sq["queries_in_flight"] == 1 and sq["steps"] == 6
