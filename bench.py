@@ -301,7 +301,7 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=16)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS),
                     help="BASELINE.json config (default c3, the headline metric's config)")
@@ -469,11 +469,16 @@ def main():
 
     def step_group(ss):
         pairs = [(j, s) for s in ss for j in range(len(queries))]
-        # (fleets of at most `fleet`, and no larger than it takes to keep every thread's group
-        # busy: a few steps dealt as one fleet would leave the other groups idle)
-        size = max(1, min(fleet, -(-len(pairs) // n_streams))) if fleets else 1
-        done = run_jobs([pairs[i:i + size] for i in range(0, len(pairs), size)] if fleets
-                        else pairs)
+        # fleets of at most `fleet`, as equal as the pairs allow and a multiple of the threads
+        # in number, so that every thread's group stays busy to the end (10 steps in fleets of
+        # 4 on two threads: 3 + 2 + 3 + 2, not 4 + 4 + 2 with one thread idle at the end)
+        if fleets:
+            nf = n_streams * -(-len(pairs) // (n_streams * fleet))
+            cut = [len(pairs) * i // nf for i in range(nf + 1)]
+            jobs = [pairs[a:b] for a, b in zip(cut, cut[1:]) if b > a]
+        else:
+            jobs = pairs
+        done = run_jobs(jobs)
         res = []
         for s in ss:
             part = [d for d in done if d[1] == s]
