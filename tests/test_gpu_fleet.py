@@ -39,7 +39,8 @@ def _begin(eng, q, n, batch):
     from torque_constrained_motion_planning_amd import _lib
     eng.set_scene(q["obs"])
     st = eng.plan_begin(START, q["goal"], q["mode"], q["mass"], 5.0, max_nodes=n + 1,
-                        max_batch=batch, seed=q["seed"])
+                        max_batch=batch, seed=q["seed"], radius=q.get("radius", 0.01),
+                        goal_probability=q.get("goal_prob", 0.2))
     assert st == _lib.PLAN_OK
 
 
@@ -106,6 +107,40 @@ def test_fleet_equals_lone_engines(k, calls, batch, n_obs, modes, masses):
         assert got[q][0] == ref[q][0], q
         assert got[q][1:4] == ref[q][1:4], q          # configs, costs, parents bit for bit
         assert got[q][4:] == ref[q][4:], q            # status, goal, counters, path, trajectory
+
+
+def test_fleet_mixed_plans():
+    """Plans that differ in everything a fleet lets them differ in: an empty scene beside
+    dense ones (64 boxes), rewire radius and goal bias per plan, and one plan that reaches its
+    goal in the first rounds while the others keep growing."""
+    from torque_constrained_motion_planning_amd.scene import obstacle_array, random_box_scene
+    plans = _plans(3, [64, 16, 32], [2, 1, 2], [5.0, 2.0, 4.0], base=301)
+    plans[1]["radius"], plans[1]["goal_prob"] = 0.5, 0.05
+    plans[2]["radius"] = 2.0
+    # an empty scene: the straight edge to the goal is free, so the goal comes at once
+    goal = plans[0]["goal"]
+    plans.append(dict(obs=np.zeros((0, 15)), goal=goal, mode=2, mass=5.0, seed=99, radius=0.3))
+    ref = _lone(plans, [9_000], 2048)
+    got = _fleet(plans, [9_000], 2048)
+    assert got == ref
+    assert ref[3][6] >= 0  # the empty-scene plan found its goal
+
+
+def test_fleet_obstacle_capacity():
+    """The fused edge kernel keeps every plan's obstacles in LDS: a fleet over ~330 of them
+    is refused with an error (the caller splits it), one within the budget runs."""
+    from torque_constrained_motion_planning_amd import _lib
+    plans = _plans(2, [40], [2], [5.0], base=17)
+    big = [dict(p) for p in plans for _ in range(5)]          # 10 plans x 40 boxes = 400
+    es = [_lib.Engine(0) for _ in big]
+    for i, (e, q) in enumerate(zip(es, big)):
+        q = dict(q, seed=q["seed"] + i)
+        _begin(e, q, 3000, 1024)
+    with pytest.raises(_lib.TcmpError):
+        _lib.plan_run_fused(es, 2000, 1024)
+    _lib.plan_run_fused(es[:8], 2000, 1024)                   # 320 obstacles: within
+    for e in es:
+        e.close()
 
 
 def test_fleet_plan_vs_oracle():
