@@ -12,8 +12,9 @@
 //     and super-cells forced to start at each plan's first node, so a plan's nodes, cells and
 //     super-cells are contiguous ranges; one k_nearest_wave32<FLEET> launch walks each
 //     candidate's own plan's super-cells (tcmp_nn32.h);
-//   - k_edges: a persistent 512-thread grid with every plan's obstacles in LDS; a wave takes
-//     one plan's edges at a time and moves on to the next plan when that queue runs dry.
+//   - the edge walk (k_fl_edges): a persistent 512-thread grid with every plan's obstacles in
+//     LDS; a wave takes one plan's edges at a time and moves on to the next plan when that
+//     queue runs dry.
 // Everything a plan computes -- its samples (its own Philox seed), nearest nodes (exact, ties
 // by its own node index), edges, node order and rewires -- is what tcmp_plan_run computes for
 // it alone: a fleet's trees are bit-identical to the lone engines' (tests/test_gpu_fleet.py).
@@ -25,8 +26,8 @@ namespace {
 
 constexpr int kFleetMax = 31;  // plans per fused round (plan ids need at most 5 key bits)
 
-// One open plan of a fused multi-plan round (tcmp_fleet.h): everything its share of a fused
-// launch reads or writes -- the plan's own buffers, so that each plan's tree is exactly the
+// One open plan of a fused multi-plan round: everything its share of a fused launch reads or
+// writes -- the plan's own buffers, so that each plan's tree is exactly the
 // one a lone engine would have grown from the same seed.
 struct FleetPlan {
   const PlanParams* P;
@@ -50,10 +51,10 @@ struct FleetPlan {
   int lds_obs;        // first row of this plan's obstacles in the fused k_edges' LDS
 };
 
-// the fused k_edges' LDS: every plan's obstacle records (f64 [n][16], then f32 [n][8]), the
-// hull geometry and one pair queue per wave of a 512-thread block
-// (behind the queues: each lane's last safe configuration, [7][512] doubles -- k_fl_edges keeps
-// it in LDS, not in 14 VGPRs: 80 -> 16 B of scratch per lane, C3 fleet edges 3.25 -> 3.16 ms)
+// k_fl_edges' LDS: every plan's obstacle records (f64 [n][16], then f32 [n][8]), the hull
+// geometry, one pair queue per wave of a 512-thread block, and behind the queues each lane's
+// last safe configuration, [7][512] doubles (in LDS, not in 14 VGPRs: 80 -> 16 B of scratch
+// per lane, C3 fleet edges 3.25 -> 3.16 ms)
 __host__ __device__ constexpr unsigned fleet_lds_bytes(int n_obs_total) {
   return scene_lds_bytes(n_obs_total) + geo_lds_bytes() + 8 * kQwaveBytes +
          7 * 512 * sizeof(double);
