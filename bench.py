@@ -102,13 +102,13 @@ WORKLOADS = {
                queries=1, scaling="weak", pipeline=3, fleet=8,
                text="C2: Panda 7-DOF, 4 axis-aligned boxes, 2 kg payload, torque_test=nov, 1e5 "
                     "batched samples per query, one query per GPU per step (queries_in_flight "
-                    "of them planned concurrently)"),
+                    "of them planned concurrently, fused_queries per fused round)"),
     "c3": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=1_000_000,
                batch=262144, alt_batch=65536, queries=1, scaling="weak", pipeline=2, fleet=4,
                text="C3: Panda 7-DOF, 16 axis-aligned boxes, 5 kg payload, torque_test=rne + "
                     "min-jerk v/a validation, 1e6 samples per query, one query per GPU per step "
-                    "(queries_in_flight of them planned concurrently; config_single_query = one "
-                    "at a time)"),
+                    "(queries_in_flight of them planned concurrently, fused_queries per fused "
+                    "round; config_single_query = one at a time)"),
     "c4": dict(boxes=16, meshes=0, mode=_lib.TORQUE_RNE, mass=5.0, samples=100_000, batch=65536,
                queries=64, scaling="strong", pipeline=3, fleet=16,
                text="C4: 64 independent start/goal queries (16 boxes each, 5 kg, rne, 1e5 "
