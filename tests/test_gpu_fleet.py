@@ -145,9 +145,9 @@ def test_fleet_obstacle_capacity():
 
 def test_fleet_index_past_lds():
     """A fleet whose joint index has more super-cells than the scan keeps in LDS (2,048:
-    sixteen plans of ~400k nodes, ~200 super-cells each): the scan walks each plan's blocks of super-cells from global
-    memory, the blocks at a plan's ends shared with its neighbours -- still every plan's lone
-    tree."""
+    sixteen plans of ~400k nodes, ~200 super-cells each): the scan walks each plan's blocks of
+    super-cells from global memory, the blocks at a plan's ends shared with its neighbours --
+    still every plan's lone tree."""
     plans = _plans(16, [16, 8], [2], [5.0], base=808)
     calls, batch = [400_000], 131072
     ref = _lone(plans, calls, batch)
