@@ -1,0 +1,6 @@
+set -e
+O=gpurun_out/$1; mkdir -p $O
+( time timeout -k 10 600 python -u bench.py > $O/bench_default_1.json 2> $O/bench_default_1.err ) 2> $O/time_default.txt
+timeout -k 10 600 python -u bench.py --no-cpu-baseline > $O/bench_default_2.json 2> $O/bench_default_2.err
+timeout -k 10 300 python -u bench.py --workload c2 --steps 5 --warmup 1 --no-cpu-baseline --no-alt > $O/bench_c2_s5.json 2> $O/bench_c2_s5.err
+timeout -k 10 300 python -u bench.py --workload c2 --no-cpu-baseline --no-alt > $O/bench_c2.json 2> $O/bench_c2.err

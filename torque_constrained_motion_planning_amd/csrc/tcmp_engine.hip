@@ -1352,6 +1352,10 @@ struct tcmp_handle {
   void* scene_pin = nullptr;
   size_t scene_pin_n = 0;
   hipEvent_t scene_ev = nullptr;
+  // pinned staging of a finished plan's trajectory rows (tcmp_plan_fetch: DMA copies instead of
+  // blit kernels through pageable memory), sized at plan_begin for kcap rows
+  void* fetch_pin = nullptr;
+  size_t fetch_pin_n = 0;
   int edge_split = 4;  // most lanes per edge in small rounds (environment TCMP_EDGE_SPLIT=1/2/4)
   int edge_wps = 2;    // k_edges' persistent grid, blocks per CU (environment TCMP_EDGE_WPS=1/2)
 
@@ -1966,6 +1970,7 @@ int tcmp_destroy(tcmp_handle* h) {
   if (h->dep_ev) (void)hipEventDestroy(h->dep_ev);
   if (h->scene_ev) (void)hipEventDestroy(h->scene_ev);
   if (h->scene_pin) (void)hipHostFree(h->scene_pin);
+  if (h->fetch_pin) (void)hipHostFree(h->fetch_pin);
   for (auto* b : {&h->nkeys_in, &h->skeys, &h->ckeys_in, &h->ckeys}) b->release();
   h->cs_hist.release();
   h->cs_hoff.release();
@@ -2925,6 +2930,15 @@ int plan_begin_launch(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result
     rc = rc ? rc : h->tqdd.ensure((size_t)h->kcap * 7);
     rc = rc ? rc : h->tpsg.ensure((size_t)h->kcap);
     rc = rc ? rc : h->ttau.ensure((size_t)h->kcap * 7);
+    // (grown only when a larger execution time raises kcap: the first plan of an engine)
+    const size_t fb = (size_t)h->kcap * 29 * sizeof(double);
+    if (!rc && h->fetch_pin_n < fb) {
+      if (h->fetch_pin) HIPCHK(hipHostFree(h->fetch_pin));
+      h->fetch_pin = nullptr;
+      h->fetch_pin_n = 0;
+      HIPCHK(hipHostMalloc(&h->fetch_pin, fb));
+      h->fetch_pin_n = fb;
+    }
     rc = rc ? rc : h->s0.ensure(16);
     rc = rc ? rc : h->i0.ensure(2);
     if (rc) return rc;
@@ -3672,6 +3686,28 @@ int tcmp_plan_fetch(tcmp_handle* h, double* waypoints, double* q, double* qd, do
   const long long W = (long long)h->fin_W, K = (long long)h->fin_K;
   if (waypoints && W)
     HIPCHK(hipMemcpyAsync(waypoints, h->wp.p, W * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
+  if (K && (size_t)K * 29 * sizeof(double) <= h->fetch_pin_n) {
+    // the trajectory rows through the pinned staging: one DMA per array, one host wait, then
+    // host copies into the caller's arrays
+    struct Part { double* dst; const double* src; size_t n; };
+    const Part parts[5] = {{q, h->tq.p, (size_t)K * 7}, {qd, h->tqd.p, (size_t)K * 7},
+                           {qdd, h->tqdd.p, (size_t)K * 7}, {psg, h->tpsg.p, (size_t)K},
+                           {tau, h->ttau.p, (size_t)K * 7}};
+    double* pin = static_cast<double*>(h->fetch_pin);
+    size_t off = 0;
+    for (const Part& p : parts) {
+      if (p.dst) HIPCHK(hipMemcpyAsync(pin + off, p.src, p.n * sizeof(double),
+                                       hipMemcpyDeviceToHost, h->stream));
+      off += p.n;
+    }
+    if (int rc_s = sync_stream(h)) return rc_s;
+    off = 0;
+    for (const Part& p : parts) {
+      if (p.dst) memcpy(p.dst, pin + off, p.n * sizeof(double));
+      off += p.n;
+    }
+    return 0;
+  }
   if (K) {
     if (q) HIPCHK(hipMemcpyAsync(q, h->tq.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
     if (qd) HIPCHK(hipMemcpyAsync(qd, h->tqd.p, K * 7 * sizeof(double), hipMemcpyDeviceToHost, h->stream));
