@@ -25,6 +25,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <thread>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1310,6 +1311,7 @@ struct tcmp_handle {
     PlanParams P;
   };
   Pin* pin = nullptr;
+  DBuf<unsigned char> dpin;     // the Pin block's device copy (plan_begin: one upload)
   size_t fin_W = 0, fin_K = 0;  // the finished plan's waypoint / trajectory rows (plan_fetch)
   long long kcap = 0;           // trajectory rows allocated at plan_begin (exec_time * 1000 + 2)
   int nn_cand_bits = 16;           // top key bits the candidates are sorted by
@@ -1967,6 +1969,7 @@ int tcmp_destroy(tcmp_handle* h) {
   h->nnscore.release();
   h->f_desc.release();
   h->f_off.release();
+  h->dpin.release();
   if (h->dep_ev) (void)hipEventDestroy(h->dep_ev);
   if (h->scene_ev) (void)hipEventDestroy(h->scene_ev);
   if (h->scene_pin) (void)hipHostFree(h->scene_pin);
@@ -2861,6 +2864,27 @@ namespace {
 
 // tcmp_plan_begin in two halves: everything up to the queued start / goal check and uploads,
 // then the one host wait and the status -- so that tcmp_plan_begin_many waits once for many
+// a plan's initial device state from the begin block (one upload of the handle's pinned Pin):
+// the root node (OptimalNode(start), rrt_star.py:155), the plan state and parameters
+__global__ void k_plan_init(const tcmp_handle::Pin* b, double* cfg, double* tgt, int* parent,
+                            int2* meta, DevState* st, PlanParams* dP) {
+  const int t = threadIdx.x;
+  if (t < 8) {
+    cfg[t] = b->root[t];
+    tgt[t] = b->root[t];
+  }
+  if (t == 0) {
+    parent[0] = b->m1;
+    meta[0] = b->z;
+  }
+  const unsigned* s = reinterpret_cast<const unsigned*>(&b->st);
+  unsigned* d = reinterpret_cast<unsigned*>(st);
+  for (int i = t; i < (int)(sizeof(DevState) / 4); i += blockDim.x) d[i] = s[i];
+  const unsigned* sp = reinterpret_cast<const unsigned*>(&b->P);
+  unsigned* dp = reinterpret_cast<unsigned*>(dP);
+  for (int i = t; i < (int)(sizeof(PlanParams) / 4); i += blockDim.x) dp[i] = sp[i];
+}
+
 int plan_begin_launch(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result* result) {
   if (!cfg || !result) return fail(-1, "null cfg/result");
   if (cfg->torque_mode < 0 || cfg->torque_mode > 3) return fail(-1, "unknown torque mode");
@@ -2945,35 +2969,34 @@ int plan_begin_launch(tcmp_handle* h, const tcmp_plan_cfg* cfg, tcmp_plan_result
   }
   h->fin_W = 0;
   h->fin_K = 0;
-  // one host wait: every copy is staged in the handle's pinned block
+  // one upload and one host wait: the handle's pinned block holds the start / goal rows, the
+  // root, the plan state and parameters; k_plan_init scatters them on the device
+  if (int rc2 = h->dpin.ensure(sizeof(tcmp_handle::Pin))) return rc2;
   tcmp_handle::Pin& pn = *h->pin;
   memset(pn.sg, 0, sizeof(pn.sg));
   memcpy(pn.sg, cfg->start, sizeof(double) * 7);
   memcpy(pn.sg + 8, cfg->goal, sizeof(double) * 7);
-  // collision(start) or collision(goal) (rrt_star.py:152)
-  HIPCHK(hipMemcpyAsync(h->s0.p, pn.sg, sizeof(pn.sg), hipMemcpyHostToDevice, h->stream));
-  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
-                     dim3(1), dim3(256), lds_bytes(h), h->stream, h->s0.p, 2LL, h->scene(),
-                     h->geo(), h->i0.p, 0);
-  HIPCHK(hipGetLastError());
-  HIPCHK(hipMemcpyAsync(pn.coll, h->i0.p, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
-  // root node (OptimalNode(start), rrt_star.py:155)
   memset(pn.root, 0, sizeof(pn.root));
   for (int k = 0; k < 7; ++k) pn.root[k] = cfg->start[k];
-  HIPCHK(hipMemcpyAsync(h->cfg.p, pn.root, sizeof(pn.root), hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipMemcpyAsync(h->tgt.p, pn.root, sizeof(pn.root), hipMemcpyHostToDevice, h->stream));
   pn.m1 = -1;
-  HIPCHK(hipMemcpyAsync(h->parent.p, &pn.m1, sizeof(int), hipMemcpyHostToDevice, h->stream));
   pn.z = make_int2(0, 0);
-  HIPCHK(hipMemcpyAsync(h->meta.p, &pn.z, sizeof(int2), hipMemcpyHostToDevice, h->stream));
   memset(&pn.st, 0, sizeof(pn.st));
   pn.st.n_nodes = 1;
   pn.st.goal_node = -1;
   pn.st.first_fail = -1;
   pn.st.round_goal = INT_MAX;
-  HIPCHK(hipMemcpyAsync(h->st, &pn.st, sizeof(pn.st), hipMemcpyHostToDevice, h->stream));
   pn.P = h->P;
-  HIPCHK(hipMemcpyAsync(h->dP, &pn.P, sizeof(PlanParams), hipMemcpyHostToDevice, h->stream));
+  const tcmp_handle::Pin* dpn = reinterpret_cast<const tcmp_handle::Pin*>(h->dpin.p);
+  HIPCHK(hipMemcpyAsync(h->dpin.p, &pn, sizeof(pn), hipMemcpyHostToDevice, h->stream));
+  hipLaunchKernelGGL(k_plan_init, dim3(1), dim3(128), 0, h->stream, dpn, h->cfg.p, h->tgt.p,
+                     h->parent.p, h->meta.p, h->st, h->dP);
+  // collision(start) or collision(goal) (rrt_star.py:152)
+  hipLaunchKernelGGL(h->mesh_kernels() ? k_check_configs<true> : k_check_configs<false>,
+                     dim3(1), dim3(256), lds_bytes(h), h->stream,
+                     reinterpret_cast<const double*>(h->dpin.p + offsetof(tcmp_handle::Pin, sg)), 2LL, h->scene(),
+                     h->geo(), h->i0.p, 0);
+  HIPCHK(hipGetLastError());
+  HIPCHK(hipMemcpyAsync(pn.coll, h->i0.p, 2 * sizeof(int), hipMemcpyDeviceToHost, h->stream));
   return 0;
 }
 
