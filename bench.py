@@ -412,7 +412,8 @@ def main():
     # consecutive steps' queries (each its own seed) -- with `pipe` fleets in flight, each on
     # its own group of engines
     fleet = args.fleet if args.fleet is not None else W.get("fleet", 0)
-    fleet = 0 if shared or W["meshes"] or args.self_collisions else fleet
+    # (convex-mesh scenes fuse only plans of one scene: the single-query workloads' steps)
+    fleet = 0 if shared or ((W["meshes"] or args.self_collisions) and len(queries) > 1) else fleet
     fleets = fleet > 1
     if fleets:
         n_streams = max(1, args.streams if args.streams else pipe)
@@ -582,7 +583,7 @@ def main():
     # the root, no index).  The plans of a fleet share their rounds' launches.
     launches = int(round(sum(x["launches_nearest"] / max(1, x.get("fused_plans", 0)) for x in kres)))
     scans = int(round(sum(x["launches_nn_scan"] / max(1, x.get("fused_plans", 0)) for x in kres)))
-    ek_name = "k_fl_edges" if fleets else "k_edges"
+    ek_name = ("k_fl_edges_mesh" if W["meshes"] else "k_fl_edges") if fleets else "k_edges"
     # (the fused-rounds scan's PMC entry: tools/pmc_summary.py)
     nn_key = "k_nearest_wave32@fleet" if fleets else "k_nearest_wave32"
 

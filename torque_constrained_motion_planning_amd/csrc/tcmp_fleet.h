@@ -18,8 +18,9 @@
 // Everything a plan computes -- its samples (its own Philox seed), nearest nodes (exact, ties
 // by its own node index), edges, node order and rewires -- is what tcmp_plan_run computes for
 // it alone: a fleet's trees are bit-identical to the lone engines' (tests/test_gpu_fleet.py).
-// Scope: box scenes (no meshes, no self-collision pairs) and identical distance weights and
-// scan bound (nn_cmax) across the plans; everything else may differ per plan.
+// Scope: identical distance weights and scan bound (nn_cmax) across the plans; box scenes may
+// differ per plan, convex-mesh scenes (or self-collision pairs) must be one scene for the whole
+// fleet (k_fl_edges_mesh stages the lead's); everything else may differ per plan.
 #pragma once
 
 namespace {
@@ -389,6 +390,114 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
   }
 }
 
+// The same walk over convex-mesh scenes, for fleets whose plans share one scene (replica trees
+// of one query, C5): the lead's scene is staged as k_edges<true, 1> stages it (256-thread blocks,
+// the lean LDS layout with the waves' stashes), and each lane's configuration stays in
+// registers (the mesh kernel's LDS has no room for it).  sc_g: the lead engine's scene.
+__global__ __launch_bounds__(256, TCMP_EDGE_MINW) void k_fl_edges_mesh(const FleetPlan* __restrict__ fp,
+                                                                      int K, int nb, Scene sc_g,
+                                                                      Geo g_g) {
+  extern __shared__ double tcmp_lds[];
+  Scene sc;
+  Geo g;
+  stage_lds<false>(sc_g, g_g, tcmp_lds, sc, g);
+  const int lane = lane_id();
+  const int waves = gridDim.x * (blockDim.x >> 6);
+  int plan = (int)((long long)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * K / waves);
+  typedef const __attribute__((address_space(4))) FleetPlan CFleetPlan;
+  CFleetPlan* const fc = (CFleetPlan*)(uintptr_t)fp;
+  CFleetPlan* F = fc + plan;
+  int visited = 1;
+  int e = -1, i = 0, n = 0;
+  bool done = false;
+  double q[7];
+#pragma unroll
+  for (int k = 0; k < 7; ++k) q[k] = 0.5 * (kLo[k] + kHi[k]);
+  StepStats ss = {};
+  unsigned steps = 0;
+  while (true) {
+    const bool need = !done && e < 0;
+    const uint64_t m = __ballot(need);
+    if (m) {
+      const int leader = __builtin_ctzll(m);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(&F->st->work_counter, (int)__popcll(m));
+      base = __shfl(base, leader);
+      if (need) {
+        const int my = base + (int)__popcll(m & ((1ull << lane) - 1ull));
+        if (my < nb) {
+          const double* rec = F->J.rec + 8 * (size_t)my;
+          const double4 ra = *reinterpret_cast<const double4*>(rec);
+          const double4 rb = *reinterpret_cast<const double4*>(rec + 4);
+          q[0] = ra.x; q[1] = ra.y; q[2] = ra.z; q[3] = ra.w;
+          q[4] = rb.x; q[5] = rb.y; q[6] = rb.z;
+          e = __double2loint(rb.w);
+          n = __double2hiint(rb.w);
+          i = 0;
+        } else {
+          done = true;
+        }
+      }
+    }
+    if (__ballot(!done) == 0) {
+      if (lane == 0 && steps) {
+        DevState* st = F->st;
+        atomicAdd(&st->edge_steps, (unsigned long long)steps);
+        atomicAdd(&st->pairs_tested, 10ull * (unsigned long long)sc_g.n_obs * ss.live_steps);
+        atomicAdd(&st->pairs_sat, (unsigned long long)ss.pairs_sat);
+        atomicAdd(&st->pairs_exact, (unsigned long long)ss.pairs_exact);
+      }
+      steps = 0;
+      ss = StepStats{};
+      if (visited++ == K) break;
+      plan = plan + 1 == K ? 0 : plan + 1;
+      F = fc + plan;
+      done = false;
+      continue;
+    }
+    const bool active = e >= 0;
+    bool tok = true, lim = false;
+    double cq[7], sq[7];
+    {
+      double qn[7], q2[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) qn[k] = q[k];
+      if (active) {
+        load7(F->J.to + 8 * (size_t)e, q2);
+        refine_step(qn, q2, n, i);
+      }
+#pragma unroll
+      for (int k = 0; k < 7; ++k) sincos(qn[k], &sq[k], &cq[k]);
+      lim = active && limits_violated(qn);
+    }
+    const int tm = F->P->torque_mode;
+    if (active && !lim && tm != TCMP_TORQUE_BASE) {
+      const double z[7] = {0, 0, 0, 0, 0, 0, 0};
+      const double mass = F->P->mass;
+      tok = tm == TCMP_TORQUE_DYN ? torque_ok_dyn<false>(cq, sq, z, z, mass)
+                                  : torque_ok<false>(cq, sq, z, z, mass);
+    }
+    const bool coll = collides_wave<true>(cq, sq, active && !lim && tok, sc, g, ss) || lim;
+    const bool ok = active && !coll && tok;
+    steps += (unsigned)__popcll(__ballot(active));
+    if (active) {
+      if (ok) {
+        double q2[7];
+        load7(F->J.to + 8 * (size_t)e, q2);
+        refine_step(q, q2, n, i);
+        ++i;
+      }
+      if (!ok || i == n) {
+        if (i > 0) atomicAdd(&F->J.accepted[e >> 8], 1);
+        F->J.nsafe[e] = i;
+        F->J.nsteps[e] = n;
+        store7(F->J.last + 8 * (size_t)e, q);
+        e = -1;
+      }
+    }
+  }
+}
+
 // ---- insertion and rewire ------------------------------------------------------------------
 __global__ __launch_bounds__(1024) void k_fl_ins_scan(const FleetPlan* __restrict__ fp, int nblk) {
   const FleetPlan& f = fp[blockIdx.x];
@@ -409,10 +518,11 @@ __global__ __launch_bounds__(256) void k_fl_rewire_scan(const FleetPlan* __restr
   const FleetPlan& f = fp[q];
   rewire_scan_block(f.P, f.st, f.tr, f.rwlist, f.nbr, f.ncount, b);
 }
+template <bool MESH>
 __global__ __launch_bounds__(256) void k_fl_rewire_apply(const FleetPlan* __restrict__ fp, int bpb, Geo g) {
   const int q = blockIdx.x / bpb, b = blockIdx.x - q * bpb;
   const FleetPlan& f = fp[q];
-  rewire_apply_block<false>(f.P, f.st, f.tr, f.rwlist, f.nbr, f.ncount, f.sc, g, b);
+  rewire_apply_block<MESH>(f.P, f.st, f.tr, f.rwlist, f.nbr, f.ncount, f.sc, g, b);
 }
 
 // ---- host ----------------------------------------------------------------------------------
@@ -422,6 +532,7 @@ struct Fleet {
   int bp, pb;              // lane stride per plan, plan-id key bits
   int lds_obs;             // obstacles over all plans (the fused k_edges' LDS)
   int max_obs;             // the largest plan scene (k_fl_rewire_apply's LDS)
+  bool mesh;               // mesh scenes: every plan's scene is the lead's
   FleetPlan* fp;           // device descriptors
   FleetNN* fnn;
 };
@@ -531,9 +642,16 @@ int fleet_round(const Fleet& F, int nb, long long base) {
   HIPCHK(hipGetLastError());
   const hipEvent_t ek = h->mark();
   h->span(F_EDGE_PREP, e1, ek);
-  const long long blocks = std::min<long long>(h->cu_count, ((long long)K * nb + 511) / 512);
-  hipLaunchKernelGGL(k_fl_edges, dim3((unsigned)std::max<long long>(1, blocks)), dim3(512),
-                     fleet_lds_bytes(F.lds_obs), h->stream, F.fp, K, nb, h->geo());
+  if (F.mesh) {
+    const long long cap = (long long)h->cu_count * TCMP_EDGE_MINW;
+    const long long blocks = std::min<long long>(cap, ((long long)K * nb + 255) / 256);
+    hipLaunchKernelGGL(k_fl_edges_mesh, dim3((unsigned)std::max<long long>(1, blocks)), dim3(256),
+                       lds_bytes(h), h->stream, F.fp, K, nb, h->scene(), h->geo());
+  } else {
+    const long long blocks = std::min<long long>(h->cu_count, ((long long)K * nb + 511) / 512);
+    hipLaunchKernelGGL(k_fl_edges, dim3((unsigned)std::max<long long>(1, blocks)), dim3(512),
+                       fleet_lds_bytes(F.lds_obs), h->stream, F.fp, K, nb, h->geo());
+  }
   HIPCHK(hipGetLastError());
   const hipEvent_t ee = h->mark_end(F_EDGES, ek);
   // insertion in lane order per plan, bookkeeping, rewire
@@ -542,11 +660,31 @@ int fleet_round(const Fleet& F, int nb, long long base) {
   hipLaunchKernelGGL(k_fl_ins_final, dim3(1), dim3(64), 0, h->stream, F.fp, K, nb);
   const hipEvent_t ei = h->mark_end(F_INSERT, ee);
   hipLaunchKernelGGL(k_fl_rewire_scan, pg, b256, 0, h->stream, F.fp, bpb);
-  hipLaunchKernelGGL(k_fl_rewire_apply, pg, b256, stage_lds_bytes(F.max_obs), h->stream, F.fp,
-                     bpb, h->geo());
+  if (F.mesh)
+    hipLaunchKernelGGL(k_fl_rewire_apply<true>, pg, b256, lds_bytes(h), h->stream, F.fp, bpb,
+                       h->geo());
+  else
+    hipLaunchKernelGGL(k_fl_rewire_apply<false>, pg, b256, stage_lds_bytes(F.max_obs), h->stream,
+                       F.fp, bpb, h->geo());
   HIPCHK(hipGetLastError());
   h->mark_end(F_REWIRE, ei);
   return 0;
+}
+
+// the scene every kernel of a plan sees: boxes, meshes (and their LODs and spheres) and the
+// self-collision switch, as the host uploaded them
+bool same_scene(const tcmp_handle* a, const tcmp_handle* b) {
+  bool same = a->n_box == b->n_box && a->n_mesh == b->n_mesh && a->self_coll == b->self_coll &&
+              a->box15 == b->box15 && a->mesh_v == b->mesh_v && a->mesh_p == b->mesh_p &&
+              a->mesh_e == b->mesh_e && a->mesh_voff == b->mesh_voff &&
+              a->mesh_poff == b->mesh_poff && a->mesh_eoff == b->mesh_eoff &&
+              a->mesh_box == b->mesh_box && a->user_lods == b->user_lods &&
+              a->user_sph == b->user_sph && a->use_sph == b->use_sph && a->sph_h == b->sph_h;
+  for (int i = 0; same && a->user_lods && i < 2; ++i)
+    same = a->lod_v[i] == b->lod_v[i] && a->lod_p[i] == b->lod_p[i] && a->lod_e[i] == b->lod_e[i] &&
+           a->lod_vo[i] == b->lod_vo[i] && a->lod_po[i] == b->lod_po[i] &&
+           a->lod_eo[i] == b->lod_eo[i];
+  return same;
 }
 
 }  // namespace
@@ -569,7 +707,10 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
     if (e->samples_issued != h->samples_issued)
       return fail(-1, "the fleet's plans are not at the same round");
     if (e->samples_issued + n_samples + 1 > e->P.max_nodes) return fail(-3, "tree capacity exceeded");
-    if (e->mesh_kernels()) return fail(-1, "fused rounds take box scenes only (no meshes, no self pairs)");
+    // mesh scenes (and self-collision pairs): one scene for the whole fleet, the lead's --
+    // replica trees of one query (C5)
+    if ((e->mesh_kernels() || h->mesh_kernels()) && !same_scene(e, h))
+      return fail(-1, "a fleet over convex-mesh scenes shares one scene");
     if (e->P.uniform_w != h->P.uniform_w || e->P.nn_cmax != h->P.nn_cmax ||
         memcmp(e->P.w, h->P.w, sizeof(h->P.w)) != 0)
       return fail(-1, "a fleet's plans share the distance weights");
@@ -588,7 +729,8 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
   }
   F.lds_obs = tot;
   F.max_obs = mx;
-  if (fleet_lds_bytes(tot) > 160u * 1024u)
+  F.mesh = h->mesh_kernels();
+  if (!F.mesh && fleet_lds_bytes(tot) > 160u * 1024u)
     return fail(-1, "too many obstacles over the fleet's scenes for the fused edge kernel");
   // the fleet index lives in the lead engine's index buffers (its own plan uses none of them
   // during a fused round), sized for every plan's nodes and lanes
@@ -634,10 +776,15 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
     hn[q] = FleetNN{e->cand.p, e->nn.p, e->second.p, e->nnscore.p, e->st, 0, 0};
   }
   HIPCHK(hipMemcpyAsync(h->f_desc.p, h->f_host.data(), dbytes, hipMemcpyHostToDevice, h->stream));
-  HIPCHK(hipFuncSetAttribute((const void*)k_fl_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
-                             (int)fleet_lds_bytes(tot)));
-  HIPCHK(hipFuncSetAttribute((const void*)k_fl_rewire_apply,
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_lds_bytes(mx)));
+  if (F.mesh) {
+    for (const void* k : {(const void*)k_fl_edges_mesh, (const void*)k_fl_rewire_apply<true>})
+      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(h)));
+  } else {
+    HIPCHK(hipFuncSetAttribute((const void*)k_fl_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)fleet_lds_bytes(tot)));
+    HIPCHK(hipFuncSetAttribute((const void*)k_fl_rewire_apply<false>,
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_lds_bytes(mx)));
+  }
   // the other engines' queued work (their plan_begin) comes first; they wait for the rounds
   for (int q = 1; q < n; ++q) {
     if (!hs[q]->dep_ev) HIPCHK(hipEventCreateWithFlags(&hs[q]->dep_ev, hipEventDisableTiming));
