@@ -116,7 +116,7 @@ WORKLOADS = {
                     "gathered to rank 0 over RCCL; a GPU's queries grow their trees in fused "
                     "rounds, `fleet` queries per set of kernel launches"),
     "c5": dict(boxes=0, meshes=256, mode=_lib.TORQUE_RNE, mass=5.0, samples=10_000_000,
-               batch=262144, queries=1, scaling="strong", pipeline=3,
+               batch=262144, queries=1, scaling="strong", pipeline=1, fleet=3,
                text="C5: dense clutter, 256 convex meshes (Panda link hulls scaled 0.5-1.5, "
                     "random poses), 5 kg, rne, 1e7 samples per step split over the GPUs -- "
                     "throughput mode: N independent replica trees of 1e7/N samples on the same "
@@ -332,14 +332,15 @@ def main():
     ap.add_argument("--fleet", type=int, default=None,
                     help="queries per fused round (tcmp_plan_run_fused): a step's queries (c4) or "
                          "consecutive steps' queries (c2, c3) grow their trees in one set of "
-                         "launches per round (default c2 8, c3 4, c4 16, the best of a one-box "
-                         "sweep; 0 or 1: one engine per query; box scenes only)")
+                         "launches per round (default c2 8, c3 4, c4 16, c5 3, the best of a "
+                         "one-box sweep; 0 or 1: one engine per query; a mesh scene fleets only "
+                         "one query's replica trees, whose scene is the same)")
     ap.add_argument("--pipeline", type=int, default=None,
                     help="steps in flight at once: P consecutive steps' queries run concurrently "
                          "on separate engines from host threads, so one query's host calls and "
                          "kernel tails overlap another's kernels (not with --shared-tree); "
                          "default per workload (c2 3 fleets of 8, c3 2 fleets of 4, c4 3 fleets "
-                         "of 16, c5 3 queries: the best of a one-box sweep); --pipeline 1 --fleet "
+                         "of 16, c5 1 fleet of 3: the best of a one-box sweep); --pipeline 1 --fleet "
                          "0 runs the steps one after another")
     args = ap.parse_args()
 

@@ -37,9 +37,11 @@ __device__ __forceinline__ void fk8(const double q[7], double R[9], double p[3])
   for (int k = 0; k < 3; ++k) p[k] = t[k];
 }
 
-// Solutions into sol[8][7]; returns the valid-branch mask (bit b = branch b).
-__device__ __forceinline__ unsigned ik8(const double R[9], const double p[3], double q7,
-                                        double sol[8][7]) {
+// Valid solutions written packed to out[c][7] in branch order (the loops below visit the
+// branches b = 4*i4 + 2*i6 + i2 in increasing order, so no per-branch staging array -- which
+// the compiler kept in scratch -- is needed); returns their count.
+__device__ __forceinline__ int ik8(const double R[9], const double p[3], double q7,
+                                   double* __restrict__ out) {
   constexpr double a = 0.0825, b = 0.384, d = 0.316, d1 = 0.333, a7 = 0.088, d8 = 0.107;
   constexpr double kPi = 3.141592653589793;
   double s7, c7;
@@ -59,7 +61,7 @@ __device__ __forceinline__ unsigned ik8(const double R[9], const double p[3], do
   constexpr double K0 = 2 * a * a + b * b + d * d, K1 = 2 * (b * d - a * a), K2 = 2 * a * (b + d);
   const double r4 = hypot(K1, K2), phi = atan2(K2, K1);
   const double C4 = (L2 - K0) / r4;
-  unsigned mask = 0;
+  int c = 0;
   if (!(fabs(C4) <= 1.0)) return 0;
   const double acos4 = atan2(sqrt(1.0 - C4 * C4), C4);
   const double u6x = x6[0] * u[0] + x6[1] * u[1] + x6[2] * u[2];
@@ -122,14 +124,13 @@ __device__ __forceinline__ unsigned ik8(const double R[9], const double p[3], do
           q1 = 0.0;
           q3 = atan2(x3[1], x3[0]) * (z3[2] > 0.0 ? 1.0 : -1.0);
         }
-        const int slot = 4 * i4 + 2 * i6 + i2;
-        sol[slot][0] = q1; sol[slot][1] = q2; sol[slot][2] = q3; sol[slot][3] = q4;
-        sol[slot][4] = q5; sol[slot][5] = q6; sol[slot][6] = q7;
-        mask |= 1u << slot;
+        double* o = out + 7 * c++;
+        o[0] = q1; o[1] = q2; o[2] = q3; o[3] = q4;
+        o[4] = q5; o[5] = q6; o[6] = q7;
       }
     }
   }
-  return mask;
+  return c;
 }
 
 // one lane per (pose, free value): poses n x 12 (R row-major, p), free n; out n x 8 x 7,
@@ -139,22 +140,12 @@ __global__ __launch_bounds__(256) void k_ik(const double* __restrict__ poses,
                                             double* __restrict__ out, int* __restrict__ count) {
   const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
-  double R[9], p[3], sol[8][7];
+  double R[9], p[3];
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = poses[12 * i + k];
 #pragma unroll
   for (int k = 0; k < 3; ++k) p[k] = poses[12 * i + 9 + k];
-  const unsigned m = ik8(R, p, free_q7[i], sol);
-  int c = 0;
-#pragma unroll
-  for (int s = 0; s < 8; ++s) {
-    if (m & (1u << s)) {
-#pragma unroll
-      for (int k = 0; k < 7; ++k) out[(8 * i + c) * 7 + k] = sol[s][k];
-      ++c;
-    }
-  }
-  count[i] = c;
+  count[i] = ik8(R, p, free_q7[i], out + 56 * i);
 }
 
 __global__ __launch_bounds__(256) void k_fk8(const double* __restrict__ q, long long n,
