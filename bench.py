@@ -259,8 +259,19 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
     import oracle as O
     O.set_meshes(meshes)
     t0 = time.perf_counter()
-    ref = O.rrt_run(START, goal, n_samples, obs, mode, mass, 5.0, batch=1, seed=seed, cull=2)
+    ref = O.rrt_run(START, goal, n_samples, obs, mode, mass, 5.0, batch=1, seed=seed, cull=2,
+                    tree=True)
     dt1 = time.perf_counter() - t0
+    g = int(ref["goal_node"])
+    depth = 0
+    if g >= 0:
+        n = g
+        while n > 0:
+            n = int(ref["tree_parent"][n])
+            depth += 1
+    q1 = quality([{"goal_node": g, "goal_cost": float(ref["tree_cost"][g]) if g >= 0 else 0.0,
+                   "goal_depth": depth, "launches_nearest": n_samples,
+                   "status": int(ref["status"])}])
     single = n_samples / dt1
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "scene.npz")
@@ -286,6 +297,8 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
             "cores": len(done) if multi else 1, "host_nproc": nproc,
             "usable_cores": usable_cores(), "kind": "port",
             "single_core": single,
+            # the single-core query's tree: B = 1, one sample per round
+            "quality": q1,
             # SURVEY 8d asks for all host cores: the measured per-core rate scaled to nproc
             # (a shared GPU box lets this process use only its share of them), and one GPU's
             # share of an 8-GPU node's host cores
@@ -298,7 +311,26 @@ def cpu_baseline(obs, goal, n_samples, seed, workers, mode=2, mass=5.0, meshes=N
                                        len(done), dtw)}
 
 
-def main():
+def quality(res):
+    """What the timed queries planned, beside how fast: rounds per query (one nearest / edge
+    launch set each), how many reached the goal, the goal node's cost (goal_n.cost,
+    rrt_star.py:25-27 -- the returned path's summed distance fn) and depth (edges root -> goal),
+    and the final statuses (0 ok, 2 no goal, 3 validation failure)."""
+    found = [x for x in res if x.get("goal_node", -1) >= 0]
+    costs = sorted(x["goal_cost"] for x in found)
+    st = {}
+    for x in res:
+        st[str(x["status"])] = st.get(str(x["status"]), 0) + 1
+    return {"queries": len(res),
+            "rounds_per_query": sum(x["launches_nearest"] for x in res) / max(1, len(res)),
+            "goal_rate": len(found) / max(1, len(res)),
+            "path_cost_mean": sum(costs) / len(costs) if costs else None,
+            "path_cost_median": costs[len(costs) // 2] if costs else None,
+            "goal_depth_mean": (sum(x["goal_depth"] for x in found) / len(found)) if found else None,
+            "status_counts": st}
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=16)
@@ -320,6 +352,11 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-alt", action="store_true",
                     help="skip the SURVEY 8d default-batch line (config_alt)")
+    ap.add_argument("--no-sublines", action="store_true",
+                    help="c3 on one GPU: skip the config_c4 / config_c5 sub-lines (BASELINE "
+                         "configs[3] and [4] measured in the same run, after the headline)")
+    ap.add_argument("--c5-steps", type=int, default=3,
+                    help="steps of the config_c5 sub-line (one fleet of three 1e7-sample trees)")
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--self-collisions", action="store_true",
                     help="add the arm's self-collision pairs (off in the reference planner)")
@@ -342,14 +379,46 @@ def main():
                          "default per workload (c2 3 fleets of 8, c3 2 fleets of 4, c4 3 fleets "
                          "of 16, c5 1 fleet of 3: the best of a one-box sweep); --pipeline 1 --fleet "
                          "0 runs the steps one after another")
-    args = ap.parse_args()
+    return ap.parse_args(argv)
 
+
+SUBLINE_KEYS = ("value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "scaling", "config",
+                "roofline", "roofline_other", "quality", "kernel_ms_per_step", "kernel_timing",
+                "host_ms_per_step", "stats_last_step")
+
+
+def main():
+    args = parse_args()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     gpu = int(os.environ.get("LOCAL_RANK", "0"))
     # one process per GPU; the collectives are libtcmp.so's RCCL communicator (no torch)
     comm = shard.comm_from_env(device=gpu) if world > 1 else None
+    line = measure(args, world, rank, gpu, comm)
+    # BASELINE configs[3] (C4, 64 queries) and configs[4] (C5, 256 meshes, 1e7 samples) in the
+    # same default run, after the headline and its CPU baseline, so the driver's own run times
+    # them too: each a full bench line of its workload (its own engines, warmup, timed steps and
+    # rooflines), condensed; one GPU only (at N > 1 run --workload c4 / c5 for the sharded form)
+    default_c3 = (args.workload == "c3" and args.samples is None and args.batch is None and
+                  args.obstacles is None and not args.shared_tree and not args.self_collisions)
+    if world == 1 and default_c3 and not args.no_sublines:
+        for wl, steps in (("c4", args.steps), ("c5", args.c5_steps)):
+            sub = parse_args(["--workload", wl, "--steps", str(max(1, steps)), "--warmup",
+                              str(min(1, args.warmup)), "--no-cpu-baseline", "--no-alt"])
+            try:
+                sl = measure(sub, world, rank, gpu, comm)
+                line["config_%s" % wl] = {k: sl[k] for k in SUBLINE_KEYS if k in sl}
+            except Exception as e:  # the headline stands; the sub-line says what failed
+                line["config_%s" % wl] = {"error": "%s: %s" % (type(e).__name__, e)}
+            log("sub-line %s done" % wl)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if comm is not None:
+        comm.close()
 
+
+def measure(args, world, rank, gpu, comm):
+    """One workload's bench line (a dict; printed by main on rank 0)."""
     W = dict(WORKLOADS[args.workload])
     if args.samples is not None:
         W["samples"] = args.samples
@@ -430,13 +499,19 @@ def main():
     if n_streams > 1:
         from concurrent.futures import ThreadPoolExecutor
         pool = ThreadPoolExecutor(n_streams)
+    # one fleet at a time (c5): no launch overlaps another's, so the fleet's lead engine keeps
+    # its event timing through the timed steps and those give the per-kernel figures (no
+    # second pass of 1e7-sample fleets)
+    lead_timed = fleets and n_streams == 1
     if n_engines > 1:
-        # concurrent queries: no per-family event timing (an overlapped launch's span includes
-        # its neighbours' kernels, and the round graphs then hold kernel nodes only; fused
+        # concurrent queries: no per-family event timing (an overlapped launch's span would
+        # include its neighbours' kernels, and the round graphs then hold kernel nodes only; fused
         # rounds record none); the per-kernel figures come from the one-at-a-time pass after
         # the timed region
         for e in engines:
             e.set_timing(False)
+        if lead_timed:
+            engines[0].set_timing(True)
 
     def run_jobs(jobs):
         """jobs: (query index, step) pairs, or lists of them (fleets).  Each engine's thread
@@ -534,7 +609,7 @@ def main():
     # one-query-at-a-time throughput (config_single_query), same build, same box.
     kres = results
     single = None
-    if fleets:
+    if fleets and not lead_timed:
         # fused rounds: S fleets one at a time on one group of engines, timed on its first
         # engine (the fleet's kernel times are reported there; every plan counts the rounds);
         # a fleet = the first `fleet` (query, step) pairs' queries, fresh seeds
@@ -695,7 +770,9 @@ def main():
                                        "+ 176 B per trajectory row, whole job"},
         "measured_peaks": measured,
         "kernel_ms_per_step": kernel_ms,
-        "kernel_timing": ("%d fleets of %d queries run one at a time after the timed steps, "
+        "kernel_timing": ("the timed steps: one fleet of %d queries at a time, kernel times on "
+                          "its lead engine, kernel_ms per step (query)" % fleet if lead_timed else
+                          "%d fleets of %d queries run one at a time after the timed steps, "
                           "kernel_ms per fleet (fleets in flight run untimed per kernel)" % (
                               S, fleet) if fleets else
                           "%d queries run one at a time on one engine after the timed steps "
@@ -709,6 +786,8 @@ def main():
         "stats_last_step": {k: results[-1][k] for k in ("status", "n_nodes", "n_waypoints", "n_traj",
                                                         "edge_steps", "pairs_tested", "pairs_sat",
                                                         "pairs_exact")},
+        # rank 0's timed queries: rounds, goal rate, path cost / depth, statuses
+        "quality": quality(results),
     }
     if comm is not None:
         # proof of the collective world the run used: RCCL's own rank count, and rank 0's check
@@ -755,19 +834,17 @@ def main():
             "ms_per_step": dta / args.steps * 1e3,
             "edge_steps_per_sample": sum(x["edge_steps"] for x in alt_res) /
             max(1, sum(x["n_samples"] for x in alt_res)),
+            "quality": quality(alt_res),
             "note": "SURVEY 8d default batch; the headline line runs batch_per_round %d" % W["batch"]}
         line["config"]["edge_steps_per_sample"] = steps / max(1.0, float(
             sum(x["n_samples"] for x in kres)))
     if single is not None:
         line["config_single_query"] = single
-    if rank == 0:
-        print(json.dumps(line), flush=True)
-    if comm is not None:
-        comm.close()
     if pool is not None:
         pool.shutdown(wait=True)
     for e in reversed(engines):  # every engine released explicitly, the first one last
         e.close()
+    return line
 
 
 if __name__ == "__main__":

@@ -236,6 +236,9 @@ typedef struct {
                              on its first engine, every plan counts the fleet's rounds */
   double ms_edge_prep;    /* the edge order's sort and work records before k_edges (ms_edges
                              times k_edges alone) */
+  double goal_cost;       /* goal_n.cost (rrt_star.py:25-27: the path's summed distance fn)
+                             when a goal node exists, else 0 */
+  int64_t goal_depth;     /* edges root -> goal node (len(retrace nodes) - 1), else 0 */
 } tcmp_plan_result;
 
 /* start a query: checks collision(start), collision(goal) (rrt_star.py:152), allocates the
@@ -269,8 +272,11 @@ int tcmp_plan_run_group(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
  * of kernel launches per round serves every plan's lanes (tcmp_fleet.h), on hs[0]'s stream;
  * the other engines' streams are ordered before and after it.  Every plan's tree is
  * bit-identical to what tcmp_plan_run(hs[q], n_samples, batch) grows alone; finish and fetch
- * each plan on its own engine as usual.  Box scenes only (no meshes, no self-collision pairs);
- * the plans must share the distance weights.  The multi-query form of tcmp_plan_run
+ * each plan on its own engine as usual.  Box scenes may differ per plan; a fleet over convex
+ * meshes or with self-collision pairs must be ONE scene (every plan's the lead's: replica trees
+ * of one query), otherwise the call returns -1.  The plans must share the distance weights, at
+ * most ~330 box obstacles over all plans (the fused edge kernel's LDS), and fewer than 2^31
+ * node / lane slots over the fleet.  The multi-query form of tcmp_plan_run
  * (collect_data.py:74-85 plans several start/goal queries per scene step). */
 int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, int32_t batch);
 

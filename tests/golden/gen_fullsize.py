@@ -23,7 +23,11 @@ C4's per-GPU shape at N = 8 (c4: eight queries bench.make_query(1234 + q), q = 0
 5 kg, rne, 1e5 samples each at B = 65,536, sample seed 5000 + q) -- the GPU test plans them on
 eight engines from eight host threads at once, as bench.py's C4 does.
 
-    python tests/golden/gen_fullsize.py [c3] [c5] [c5b] [c4]
+C2 (c2: bench.py make_query(1234) on the C2 workload -- 4 boxes, 2 kg, nov -- 1e5 samples at
+B = 65,536, seed 1234 = step_seed(0) of rank 0): the bench's own C2 query, which the GPU test
+plans as one plan of the bench's fleet of eight.
+
+    python tests/golden/gen_fullsize.py [c3] [c5] [c5b] [c4] [c2]
 """
 import hashlib
 import os
@@ -120,21 +124,21 @@ def make_c4(n_q=8, samples=100_000, batch=65536):
           flush=True)
 
 
-def make(name, n_obs, n_mesh, samples, batch, seed):
+def make(name, n_obs, n_mesh, samples, batch, seed, mode=2, mass=5.0):
     import bench
     eng = OracleEngine()
-    obs, pack, goal = bench.make_query(1234, n_obs=n_obs, mode=2, mass=5.0, engine=eng,
+    obs, pack, goal = bench.make_query(1234, n_obs=n_obs, mode=mode, mass=mass, engine=eng,
                                        n_mesh=n_mesh)
     O.set_meshes(pack)
     t0 = time.time()
-    ref = O.rrt_run(START, goal, samples, obs if len(obs) else None, 2, 5.0, 5.0, batch=batch,
+    ref = O.rrt_run(START, goal, samples, obs if len(obs) else None, mode, mass, 5.0, batch=batch,
                     seed=seed, cull=2, threads=THREADS, tree=True)
     dt = time.time() - t0
     O.set_meshes(None)
     K = ref["n_traj"]
     sel = np.arange(0, K, TRAJ_STRIDE)
     out = dict(obs=obs, goal=goal, samples=samples, batch=batch, seed=seed, n_mesh=n_mesh,
-               status=ref["status"], n_nodes=ref["n_nodes"], n_samples=ref["n_samples"],
+               mode=mode, mass=mass, status=ref["status"], n_nodes=ref["n_nodes"], n_samples=ref["n_samples"],
                edge_steps=ref["edge_steps"], goal_node=ref["goal_node"],
                n_waypoints=ref["n_waypoints"], n_traj=K, first_fail=ref["first_fail"],
                n_rewires=ref["n_rewires"], waypoints=ref["waypoints"], traj_sel=sel,
@@ -153,7 +157,7 @@ def make(name, n_obs, n_mesh, samples, batch, seed):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["c3", "c5", "c5b", "c4"]
+    which = sys.argv[1:] or ["c3", "c5", "c5b", "c4", "c2"]
     if "c3" in which:
         make("c3", 16, 0, 1_000_000, 262144, 1234)
     if "c5" in which:
@@ -162,3 +166,5 @@ if __name__ == "__main__":
         make("c5b", 0, 256, 2 * 262144 + 38528, 262144, 1234)
     if "c4" in which:
         make_c4()
+    if "c2" in which:
+        make("c2", 4, 0, 100_000, 65536, 1234, mode=1, mass=2.0)

@@ -63,6 +63,7 @@ class _FakeEngine:
         r.nn_pairs, r.nn_full_pairs, r.snap_sum = 800 * self.n, self.n * self.n, self.n
         r.ms_nearest, r.ms_nn_scan, r.ms_edges = 5.0, 4.0, 4.5
         r.launches_nearest, r.launches_nn_scan = 4, 3
+        r.goal_node, r.goal_cost, r.goal_depth = self.n // 2 - 1, 3.5, 4
         return r
 
     def plan_fetch(self, r):
@@ -156,7 +157,7 @@ def test_bench_single_query_fleets(monkeypatch, capsys):
     `fleet`, `pipeline` fleets in flight; the one-query-at-a-time line rides beside it."""
     line = _run_bench(monkeypatch, capsys, ["--workload", "c3", "--steps", "6", "--warmup", "1",
                                             "--fleet", "4", "--pipeline", "2",
-                                            "--no-cpu-baseline", "--no-alt"])
+                                            "--no-cpu-baseline", "--no-alt", "--no-sublines"])
     c = line["config"]
     assert c["fused_queries"] == 4 and c["queries_in_flight"] == 8 and c["streams_per_gpu"] == 8
     # warmup 1 x 2 x 4 = 8 steps (2 fleets of 4), timed 6 steps (two fleets of 3: one per
@@ -183,3 +184,34 @@ def test_bench_multi_query_pipeline(monkeypatch, capsys):
     # kernel-timing queries; every seed distinct
     assert len(_FakeEngine.seeds) == 15 and len(set(_FakeEngine.seeds)) == 15
     assert line["value"] == pytest.approx(3 * 2 * 100_000 / (line["ms_per_step"] * 2e-3), rel=1e-6)
+
+
+def test_bench_default_sublines(monkeypatch, capsys):
+    """The default c3 command also measures BASELINE configs[3] (config_c4) and configs[4]
+    (config_c5) after the headline, each a full line of its workload condensed into a sub-line
+    (its own warmup, timed steps, rooflines and plan quality).  C5's one fleet in flight keeps
+    event timing on its lead engine, so its kernel figures come from the timed steps (no second
+    pass of 1e7-sample fleets)."""
+    import bench
+    small = dict(bench.WORKLOADS)
+    small["c4"] = dict(small["c4"], queries=4, fleet=2, pipeline=2, samples=2000)
+    small["c5"] = dict(small["c5"], meshes=2, samples=3000)
+    monkeypatch.setattr(bench, "WORKLOADS", small)
+    line = _run_bench(monkeypatch, capsys, ["--steps", "2", "--warmup", "1", "--samples", "5000",
+                                            "--no-cpu-baseline", "--no-alt"])
+    # --samples: not the default headline, so no sub-lines
+    assert "config_c4" not in line and "config_c5" not in line
+    small["c3"] = dict(small["c3"], samples=5000)
+    line = _run_bench(monkeypatch, capsys, ["--steps", "2", "--warmup", "1", "--c5-steps", "3",
+                                            "--no-cpu-baseline", "--no-alt"])
+    q = line["quality"]
+    assert q["queries"] == 2 and q["goal_rate"] == 1.0 and q["path_cost_mean"] == 3.5
+    assert q["rounds_per_query"] == 4 and q["goal_depth_mean"] == 4
+    c4, c5 = line["config_c4"], line["config_c5"]
+    assert "error" not in c4 and "error" not in c5, (c4, c5)
+    assert c4["steps"] == 2 and c4["config"]["queries_per_step"] == 4 and c4["value"] > 0
+    assert c4["config"]["fused_queries"] == 2 and "roofline" in c4 and "quality" in c4
+    assert c5["steps"] == 3 and c5["config"]["meshes"] == 2 and c5["config"]["fused_queries"] == 3
+    assert c5["kernel_timing"].startswith("the timed steps")
+    assert c5["roofline"]["avg_launch_ms"] > 0 and c5["quality"]["queries"] == 3
+    assert "cpu_baseline" not in c4 and "config_alt" not in c5

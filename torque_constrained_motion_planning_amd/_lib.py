@@ -76,6 +76,7 @@ class PlanResult(ctypes.Structure):
         ("launches_nn_scan", ctypes.c_int64), ("n_rewires", ctypes.c_uint64),
         ("rewire_steps", ctypes.c_uint64), ("graph_launches", ctypes.c_int64),
         ("fused_plans", ctypes.c_int64), ("ms_edge_prep", ctypes.c_double),
+        ("goal_cost", ctypes.c_double), ("goal_depth", ctypes.c_int64),
     ]
 
     def as_dict(self):

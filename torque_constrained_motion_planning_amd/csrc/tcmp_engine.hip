@@ -156,6 +156,8 @@ struct DevState {
                          // the lower ranks' accepted edges in a shared-tree round)
   long long ins_all;     // accepted edges of the round over all ranks (ins_total alone)
   long long ins_goal;    // lowest goal-reaching new node of the round (k_ins_write)
+  double goal_cost;      // the goal node's cost and depth (k_retrace)
+  long long goal_depth;
   int work_counter;
   int nn_counter;
   int round_goal;
@@ -916,6 +918,8 @@ __global__ __launch_bounds__(256) void k_retrace(const PlanParams* __restrict__ 
     const long long cap = st->n_nodes;
     for (long long n = goal; n > 0 && L < cap; n = tr.parent[n]) chain[L++] = n;
     sL = L;
+    st->goal_cost = tr.cfg[8 * goal + 7];
+    st->goal_depth = L;
   }
   __syncthreads();
   const long long L = sL;
@@ -1795,6 +1799,7 @@ PlanParams default_params() {
 }
 
 int upload_spheres(tcmp_handle* h);  // (below) the links' and meshes' inscribed spheres
+int fleet_lds_limits();  // (tcmp_fleet.h) the fused kernels' dynamic-LDS limits, set once
 }  // namespace
 
 // ==========================================================================================
@@ -1917,6 +1922,7 @@ int tcmp_create(int device, tcmp_handle** out) {
                           (const void*)k_check_configs<false>, (const void*)k_check_configs<true>,
                           (const void*)k_rewire_apply<false>, (const void*)k_rewire_apply<true>})
       HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, lim));
+    if (int rc2 = fleet_lds_limits()) { delete h; return rc2; }
   }
   HIPCHK(hipMalloc(&h->st, sizeof(DevState)));
   HIPCHK(hipMemset(h->st, 0, sizeof(DevState)));
@@ -3025,9 +3031,19 @@ int tcmp_plan_begin_many(tcmp_handle* const* hs, int32_t n, const tcmp_plan_cfg*
   Entry entry;
   if (!hs || n < 1 || !cfgs || !results) return fail(-1, "bad arguments");
   for (int q = 0; q < n; ++q) {
-    if (int rc = set_dev(hs[q])) return rc;
-    if (int rc = plan_begin_launch(hs[q], cfgs + q, results + q))
-      return fail(rc, "plan " + std::to_string(q) + ": " + tcmp_last_error());
+    int rc = set_dev(hs[q]);
+    rc = rc ? rc : plan_begin_launch(hs[q], cfgs + q, results + q);
+    if (rc) {
+      // the engines already launched have begin work queued (the device-to-host copy into
+      // their pinned block among it): wait for it, so that no later begin rewrites that block
+      // while the copy is pending; their plans stay closed
+      const std::string why = "plan " + std::to_string(q) + ": " + tcmp_last_error();
+      for (int p = 0; p < q; ++p) {
+        if (set_dev(hs[p]) == 0) (void)sync_stream(hs[p]);
+        hs[p]->plan_open = false;
+      }
+      return fail(rc, why);
+    }
   }
   for (int q = 0; q < n; ++q) {
     if (int rc = set_dev(hs[q])) return rc;
@@ -3667,6 +3683,8 @@ static int plan_finish_complete(tcmp_handle* h, tcmp_plan_result* r, bool traj) 
   r->ms_nn_scan = h->ms[F_NNSCAN];
   r->ms_edge_prep = h->ms[F_EDGE_PREP];
   r->fused_plans = h->fused_plans;
+  r->goal_cost = s.goal_node >= 0 ? s.goal_cost : 0.0;
+  r->goal_depth = s.goal_node >= 0 ? s.goal_depth : 0;
   r->snap_sum = s.snap_sum;
   r->nn_full_pairs = s.nn_full_pairs;
   r->n_rewires = s.rewires;

@@ -26,6 +26,7 @@
 namespace {
 
 constexpr int kFleetMax = 31;  // plans per fused round (plan ids need at most 5 key bits)
+constexpr unsigned kFleetLdsCap = 160u * 1024u;  // k_fl_edges' LDS (a CU's whole 160 KB)
 
 // One open plan of a fused multi-plan round: everything its share of a fused launch reads or
 // writes -- the plan's own buffers, so that each plan's tree is exactly the
@@ -643,7 +644,8 @@ int fleet_round(const Fleet& F, int nb, long long base) {
   const hipEvent_t ek = h->mark();
   h->span(F_EDGE_PREP, e1, ek);
   if (F.mesh) {
-    const long long cap = (long long)h->cu_count * TCMP_EDGE_MINW;
+    // (launch_edges' residency cap, the engine's edge_wps included)
+    const long long cap = (long long)h->cu_count * std::max(1, std::min(h->edge_wps, TCMP_EDGE_MINW));
     const long long blocks = std::min<long long>(cap, ((long long)K * nb + 255) / 256);
     hipLaunchKernelGGL(k_fl_edges_mesh, dim3((unsigned)std::max<long long>(1, blocks)), dim3(256),
                        lds_bytes(h), h->stream, F.fp, K, nb, h->scene(), h->geo());
@@ -685,6 +687,21 @@ bool same_scene(const tcmp_handle* a, const tcmp_handle* b) {
            a->lod_vo[i] == b->lod_vo[i] && a->lod_po[i] == b->lod_po[i] &&
            a->lod_eo[i] == b->lod_eo[i];
   return same;
+}
+
+// The fused kernels' dynamic-LDS limits, at the largest any fleet may launch them with (the
+// fleet LDS cap of k_fl_edges, the largest box / lean mesh stage): called by every
+// tcmp_create, never per fleet -- a limit is global to its function, and a per-call value
+// set by one thread could be lowered by another's smaller fleet before the first one launches.
+int fleet_lds_limits() {
+  const struct { const void* k; unsigned b; } lim[] = {
+      {(const void*)k_fl_edges, kFleetLdsCap},
+      {(const void*)k_fl_rewire_apply<false>, stage_lds_bytes(kMaxObstacles)},
+      {(const void*)k_fl_edges_mesh, stage_lds_bytes_lean(kMaxObstacles)},
+      {(const void*)k_fl_rewire_apply<true>, stage_lds_bytes_lean(kMaxObstacles)}};
+  for (const auto& x : lim)
+    HIPCHK(hipFuncSetAttribute(x.k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)x.b));
+  return 0;
 }
 
 }  // namespace
@@ -730,7 +747,7 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
   F.lds_obs = tot;
   F.max_obs = mx;
   F.mesh = h->mesh_kernels();
-  if (!F.mesh && fleet_lds_bytes(tot) > 160u * 1024u)
+  if (!F.mesh && fleet_lds_bytes(tot) > kFleetLdsCap)
     return fail(-1, "too many obstacles over the fleet's scenes for the fused edge kernel");
   // the fleet index lives in the lead engine's index buffers (its own plan uses none of them
   // during a fused round), sized for every plan's nodes and lanes
@@ -776,15 +793,8 @@ int tcmp_plan_run_fused(tcmp_handle* const* hs, int32_t n, int64_t n_samples, in
     hn[q] = FleetNN{e->cand.p, e->nn.p, e->second.p, e->nnscore.p, e->st, 0, 0};
   }
   HIPCHK(hipMemcpyAsync(h->f_desc.p, h->f_host.data(), dbytes, hipMemcpyHostToDevice, h->stream));
-  if (F.mesh) {
-    for (const void* k : {(const void*)k_fl_edges_mesh, (const void*)k_fl_rewire_apply<true>})
-      HIPCHK(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_bytes(h)));
-  } else {
-    HIPCHK(hipFuncSetAttribute((const void*)k_fl_edges, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)fleet_lds_bytes(tot)));
-    HIPCHK(hipFuncSetAttribute((const void*)k_fl_rewire_apply<false>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)stage_lds_bytes(mx)));
-  }
+  // (the kernels' dynamic-LDS limits are set once, at their largest, by tcmp_create:
+  // fleet_lds_limits)
   // the other engines' queued work (their plan_begin) comes first; they wait for the rounds
   for (int q = 1; q < n; ++q) {
     if (!hs[q]->dep_ev) HIPCHK(hipEventCreateWithFlags(&hs[q]->dep_ev, hipEventDisableTiming));
