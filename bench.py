@@ -355,6 +355,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-sublines", action="store_true",
                     help="c3 on one GPU: skip the config_c4 / config_c5 sub-lines (BASELINE "
                          "configs[3] and [4] measured in the same run, after the headline)")
+    ap.add_argument("--no-single", action="store_true",
+                    help="skip the one-query-at-a-time pass of a single-query workload "
+                         "(config_single_query; the sub-lines skip it)")
     ap.add_argument("--c5-steps", type=int, default=3,
                     help="steps of the config_c5 sub-line (one fleet of three 1e7-sample trees)")
     ap.add_argument("--verbose", action="store_true")
@@ -404,7 +407,8 @@ def main():
     if world == 1 and default_c3 and not args.no_sublines:
         for wl, steps in (("c4", args.steps), ("c5", args.c5_steps)):
             sub = parse_args(["--workload", wl, "--steps", str(max(1, steps)), "--warmup",
-                              str(min(1, args.warmup)), "--no-cpu-baseline", "--no-alt"])
+                              str(min(1, args.warmup)), "--no-cpu-baseline", "--no-alt",
+                              "--no-single"])
             try:
                 sl = measure(sub, world, rank, gpu, comm)
                 line["config_%s" % wl] = {k: sl[k] for k in SUBLINE_KEYS if k in sl}
@@ -627,7 +631,7 @@ def measure(args, world, rank, gpu, comm):
         grp[0].synchronize()
         grp[0].set_timing(False)
         barrier()
-    if n_engines > 1 and (not fleets or len(queries) == 1):
+    if n_engines > 1 and (not fleets or (len(queries) == 1 and not args.no_single)):
         e0 = engines[0]
         e0.set_timing(True)
         obs, pack, goal = queries[0]

@@ -9,9 +9,9 @@ for r in 1 2; do
   for S in $SETS; do
     i=$((i+1))
     if [ "$S" = NONE ]; then
-      timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
+      timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt --no-sublines "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
     else
-      env $S timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
+      env $S timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt --no-sublines "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
     fi
   done
 done

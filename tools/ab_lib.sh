@@ -9,7 +9,7 @@ for r in 1 2; do
   i=0
   for L in $LIBS; do
     i=$((i+1))
-    TCMP_LIB_PATH=$L timeout -k 10 200 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
+    TCMP_LIB_PATH=$L timeout -k 10 300 python -u bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-alt --no-sublines "$@" > $O/bench_${i}_$r.json 2> $O/bench_${i}_$r.err
   done
 done
 echo done > $O/DONE
