@@ -16,6 +16,7 @@
 #   valu[=W]         PMC pass of the SQ_INSTS_VALU_* / FLOPS counters over one bench step
 #   mix[=W]          PMC pass of the instruction mix (SQ_INSTS total / VALU / SALU / branch /
 #                    LDS / VMEM / SMEM, SQ_THREAD_CYCLES_VALU) over one bench step
+#   meshprof[=N]     profiling build (make prof): tools/mesh_profile.py on C5 (N samples, 1e6)
 #   prof             profiling-build (make prof) clock breakdowns: tools/nn_profile.py and
 #                    tools/edge_profile.py on C3
 #   ab=LIBS          same-box A/B of libtcmp builds (space-separated .so paths): C3 bench lines,
@@ -26,6 +27,8 @@
 #   line=W:ARGS      one bench line of workload W with extra bench arguments (commas for spaces),
 #                    e.g. line=c5:--steps,6,--fleet,3 ; output line_W_<n>.json
 #   abw=W            ab (the TCMP_LIB_PATH builds listed in env:AB_LIBS) on workload W
+#   abenv=W          same-box A/B of environment settings (env:AB_SETS="VAR=a VAR=b", NONE for
+#                    none) on workload W, two passes (tools/ab_env.sh)
 #   env:VAR=V        export VAR=V for the following stages (A/B knobs, TCMP_LIB_PATH=...)
 # Outputs under gpurun_out/TAG/.
 set -e -o pipefail
@@ -39,6 +42,7 @@ pmc_args() {  # workload -> bench.py arguments of a counter pass: whole fleets, 
   case "$1" in
     c3|"") echo "--steps 4 --warmup 0 --pipeline 1 --no-sublines" ;;   # one fleet of 4 (+ the timing pass's)
     c2) echo "--workload c2 --steps 8 --warmup 0 --pipeline 1" ;;
+    c5) echo "--workload c5 --steps 3 --warmup 0 --pipeline 1 --no-single" ;;   # one fleet of 3
     *) echo "--workload $1 --steps 1 --warmup 0 --pipeline 1" ;;
   esac
 }
@@ -116,6 +120,9 @@ for st in "$@"; do
       P=torque_constrained_motion_planning_amd/libtcmp_prof.so
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/nn_profile.py 2 > $O/nn_profile.json 2> $O/nn_profile.err
       TCMP_LIB_PATH=$P timeout -k 10 200 python -u tools/edge_profile.py 2 > $O/edge_profile.json 2> $O/edge_profile.err ;;
+    meshprof)
+      TCMP_LIB_PATH=torque_constrained_motion_planning_amd/libtcmp_prof.so timeout -k 10 300 \
+        python -u tools/mesh_profile.py ${arg:-1000000} > $O/mesh_profile.json 2> $O/mesh_profile.err ;;
     ab)
       bash tools/ab_lib.sh $TAG/ab "$arg" ${AB_ARGS:-} ;;
     sweep)
@@ -132,6 +139,8 @@ for st in "$@"; do
       timeout -k 10 600 python -u bench.py --workload $w ${extra//,/ } > $O/line_${w}_$nl.json 2> $O/line_${w}_$nl.err ;;
     abw)
       bash tools/ab_lib.sh $TAG/ab_$arg "${AB_LIBS:?env:AB_LIBS=...}" --workload $arg --no-sublines ${AB_ARGS:-} ;;
+    abenv)
+      bash tools/ab_env.sh $TAG/abenv_$arg "${AB_SETS:?env:AB_SETS=...}" --workload $arg ${AB_ARGS:-} ;;
     c5seeds)
       timeout -k 10 300 python -u tools/c5_fixture_search.py ${arg//,/ } > $O/c5seeds.jsonl 2> $O/c5seeds.err ;;
     env:*)
