@@ -1300,7 +1300,7 @@ struct tcmp_handle {
   DBuf<unsigned long long> ckey;
   DBuf<unsigned char> sort_tmp;
   DevState* st_nn = nullptr;  // state of tcmp_nearest's standalone index (keeps a plan's intact)
-  int nn_waves_per_cu = 16;
+  int nn_waves_per_cu = (kNnBlock / 64) * TCMP_NN_MINB;  // the scan's resident waves per CU
   hipEvent_t ins_ev = nullptr;     // open F_INSERT mark between round_search and round_finish
   DBuf<long long> xch;             // shared-tree round exchange slots (k_sr_*)
   DBuf<int> cs_hist, cs_hoff;      // counting-sort histogram (kept zeroed) and bin offsets
