@@ -1029,7 +1029,11 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   const float po = exact_pd_wave32(link, pose(), ob, g);
   TCMP_MESH_CLK(0);
   if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
-  if (rg[18]) {
+  // The outer-LOD "free" stage runs only without the sphere certificates: with them, the pairs
+  // that reach the chain are mostly ones the outer LODs cannot prove free (~15 %), and the
+  // full hulls' facet passes prove those anyway -- dropping the stage: C5 edges -10 %, same-box
+  // A/B (profiles/r9g_ab_c5_chain).
+  if (rg[18] && !inner_first) {
     const HullA32 Ao{sc.lodv3[1], sc.lodpl[1], sc.lodei[1], sc.lodev[1], tcmp_lod_out_vert_off[link],
                      tcmp_lod_out_vert_off[link + 1], tcmp_lod_out_plane_off[link],
                      tcmp_lod_out_plane_off[link + 1], tcmp_lod_out_edge_off[link],
@@ -1045,6 +1049,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
       if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
     }
   } else {
+    // the mesh's inner box ("collision" above kPen + guard): meshes without LODs, and after the
+    // inner LOD with the sphere certificates on (as measured in the A/B above)
     const double* ib = sc.mib + 16 * mi;
     if (ib[12] > 0.0) {
       const float pi = exact_pd_wave32(link, pose(), ib, g);
@@ -1061,7 +1067,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;
   TCMP_MESH_STAT(7);
   const double r64 = exact_mesh_wave(link, pose_to_lds(), mi, sc.mrange, sc.mp64, sc.mv64, sc.me64,
-                                     g.verts, g.planes, g.edges);
+                                     sc.mcl, g.verts, g.planes, g.edges);
   TCMP_MESH_CLK(4);
   return r64;
 #undef TCMP_MESH_STAT

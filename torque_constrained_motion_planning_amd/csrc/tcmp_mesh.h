@@ -291,11 +291,15 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
 // fp64 restatement of hull_hull_wave32 on the full hulls (same axes, strict Gauss-map test, no degeneracy
 // shortcuts): the decision-maker near kPen.  Every lane of the wave calls it.
 // pose: R[9], p[3] in the wave's LDS pose slot; pointers one by one (no argument in scratch)
+// The edge pairs are pruned by the mesh's Gauss-map clusters exactly as in hull_hull_wave32
+// (a cluster whose cone cannot meet the lane's arc holds no intersecting arc; the cones are
+// conservative by kConeSlack), so the minimum is the unpruned one.
 __device__ __noinline__ double exact_mesh_wave(int link, const double* pose, int m,
                                                const int* __restrict__ mrange,
                                                const double4* __restrict__ mp64,
                                                const double4* __restrict__ mv64,
                                                const double* __restrict__ me64,
+                                               const float4* __restrict__ mcl,
                                                const double* __restrict__ gverts,
                                                const double* __restrict__ gplanes,
                                                const double* __restrict__ gedges) {
@@ -357,19 +361,34 @@ __device__ __noinline__ double exact_mesh_wave(int link, const double* pose, int
     const double px = R[0] * L[4] + R[1] * L[5] + R[2] * L[6] + p[0];
     const double py = R[3] * L[4] + R[4] * L[5] + R[5] * L[6] + p[1];
     const double pz = R[6] * L[4] + R[7] * L[5] + R[8] * L[6] + p[2];
-    for (int k = e0; k < e1; ++k) {
-      const double* E = sc.me64 + 16 * k;
-      const double cba = E[0] * ux + E[1] * uy + E[2] * uz;
-      const double dba = E[3] * ux + E[4] * uy + E[5] * uz;
-      if (!(cba * dba < 0)) continue;
-      const double adc = ax * E[6] + ay * E[7] + az * E[8];
-      const double bdc = bx * E[6] + by * E[7] + bz * E[8];
-      if (!(adc * bdc < 0 && cba * bdc > 0)) continue;
-      double n0 = ey * E[11] - ez * E[10], n1 = ez * E[9] - ex * E[11], n2 = ex * E[10] - ey * E[9];
-      const double len2 = n0 * n0 + n1 * n1 + n2 * n2;
-      if (len2 < 1e-24) continue;
-      if (n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz) < 0) { n0 = -n0; n1 = -n1; n2 = -n2; }
-      loc = fmin(loc, (n0 * (px - E[12]) + n1 * (py - E[13]) + n2 * (pz - E[14])) / sqrt(len2));
+    // the lane's arc a -> b in its cone (unit(a + b), half the a-b angle), fp32
+    const double sx = ax + bx, sy = ay + by, sz = az + bz;
+    const double s2 = sx * sx + sy * sy + sz * sz;
+    const bool knife = !(s2 > 1e-6);  // antipodal normals: no cone, every cluster
+    const float is = knife ? 0.f : (float)(1.0 / sqrt(s2));
+    const float qx = (float)sx * is, qy = (float)sy * is, qz = (float)sz * is;
+    const double cab = ax * bx + ay * by + az * bz;
+    const float ca = (float)sqrt(fmax(0.0, 0.5 * (1.0 + cab))), sa = (float)sqrt(fmax(0.0, 0.5 * (1.0 - cab)));
+    for (int c = rg[20]; c < rg[21]; ++c) {
+      const float4 cw = mcl[2 * c], cs = mcl[2 * c + 1];
+      if (!knife && !(cw.w <= -ca + kConeSlack ||
+                      qx * cw.x + qy * cw.y + qz * cw.z >= ca * cw.w - sa * cs.x - kConeSlack))
+        continue;
+      const int k1 = __float_as_int(cs.z);
+      for (int k = __float_as_int(cs.y); k < k1; ++k) {
+        const double* E = sc.me64 + 16 * k;
+        const double cba = E[0] * ux + E[1] * uy + E[2] * uz;
+        const double dba = E[3] * ux + E[4] * uy + E[5] * uz;
+        if (!(cba * dba < 0)) continue;
+        const double adc = ax * E[6] + ay * E[7] + az * E[8];
+        const double bdc = bx * E[6] + by * E[7] + bz * E[8];
+        if (!(adc * bdc < 0 && cba * bdc > 0)) continue;
+        double n0 = ey * E[11] - ez * E[10], n1 = ez * E[9] - ex * E[11], n2 = ex * E[10] - ey * E[9];
+        const double len2 = n0 * n0 + n1 * n1 + n2 * n2;
+        if (len2 < 1e-24) continue;
+        if (n0 * (ax + bx) + n1 * (ay + by) + n2 * (az + bz) < 0) { n0 = -n0; n1 = -n1; n2 = -n2; }
+        loc = fmin(loc, (n0 * (px - E[12]) + n1 * (py - E[13]) + n2 * (pz - E[14])) / sqrt(len2));
+      }
     }
   }
   return fmin(pd, wave_min(loc));
