@@ -20,7 +20,7 @@ def main():
     eng = _lib.Engine(0)
     obs, pack, goal = bench.make_query(1234, n_obs=0, n_mesh=W["meshes"], engine=eng)
     r, _ = bench.run_query(eng, obs, goal, n, W["batch"], 1234, meshes=pack)
-    c = eng.debug_counters(52)
+    c = eng.debug_counters(84)
     tot = max(1, c[0])
     print(json.dumps({"samples": n, "ms_edges": r.ms_edges, "ms_nearest": r.ms_nearest,
                       "edge_steps": r.edge_steps, "pairs_tested": r.pairs_tested,
@@ -36,6 +36,11 @@ def main():
                       "hull_hull_exits": {"mesh_facets": c[20], "link_facets": c[21],
                                           "edges_early": c[22], "full_collision": c[23],
                                           "full_free": c[24], "degenerate": c[25]},
+                      # the head's overlap excess fa - kPen (m) of the pairs past the head, by
+                      # the chain's verdict
+                      "head_excess_hist": {"edges_m": [0.0025, 0.005, 0.01, 0.02, 0.04, 0.08, 0.16,
+                                                       0.32, "inf", "no head", "no axis"],
+                                           "free": c[52:63], "collision": c[68:79]},
                       "mesh_stage_clk_share": dict(zip(
                           ("outer_box", "outer_lod", "inner_lod", "full_fp32", "fp64"),
                           (round(x / max(1, sum(c[28:33]) + c[46]), 4) for x in c[28:33])))}),

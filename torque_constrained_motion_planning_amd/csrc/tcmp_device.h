@@ -667,6 +667,10 @@ constexpr int max_link_edges() {
   return m;
 }
 #ifdef TCMP_PROF_EXACT
+// mesh chain pairs past the head stage by the head's overlap excess (fa - kPen: buckets of
+// 2.5 mm doubling to 32 cm, [9] no head, [10] head without an axis) and verdict ([16 + b]
+// collision)
+__device__ unsigned long long g_fa_hist[32];
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
 __device__ unsigned long long g_exact_stats[32];  // [4..7]: mesh pairs (exact_pair),
@@ -985,6 +989,12 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
 #endif
   constexpr float P = (float)kPen;
   const int* rg = sc.mrange + kMrange * mi;
+#ifdef TCMP_PROF_EXACT
+  int fab = 9;
+#define TCMP_FA_REC(v) if (lane_id() == 0) atomicAdd(&g_fa_hist[((v) >= kPen ? 16 : 0) + fab], 1ull)
+#else
+#define TCMP_FA_REC(v)
+#endif
   if (rg[19]) {
     float Rf[9], pf[3];
     {
@@ -997,6 +1007,13 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     const float fa = facet_axes_wave(link, Rf, pf, mi, rg, sc, g);
     TCMP_MESH_CLK(10);  // slot 26
     if (fa < P - kExactGuard) { TCMP_MESH_STAT(23); return (double)fa; }
+#ifdef TCMP_PROF_EXACT
+    {
+      const float e = fa - P;
+      fab = !(e < 1e30f) ? 10 : e < 0.0025f ? 0 : e < 0.005f ? 1 : e < 0.01f ? 2 : e < 0.02f ? 3
+          : e < 0.04f ? 4 : e < 0.08f ? 5 : e < 0.16f ? 6 : e < 0.32f ? 7 : 8;
+    }
+#endif
   }
   float R[9], p[3];
   {
@@ -1024,11 +1041,11 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   if (inner_first) {
     const float pi = inner_lod();
     TCMP_MESH_CLK(2);
-    if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+    if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); TCMP_FA_REC(pi); return (double)pi; }
   }
   const float po = exact_pd_wave32(link, pose(), ob, g);
   TCMP_MESH_CLK(0);
-  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); return (double)po; }
+  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); TCMP_FA_REC(po); return (double)po; }
   // The outer-LOD "free" stage runs only without the sphere certificates: with them, the pairs
   // that reach the chain are mostly ones the outer LODs cannot prove free (~15 %), and the
   // full hulls' facet passes prove those anyway -- dropping the stage: C5 edges -10 %, same-box
@@ -1042,11 +1059,11 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
                      sc.lcl[1], rg[24], rg[25]};
     const float pl = hull_hull_wave32<false>(Ao, Bo, R, p, P - kExactGuard);
     TCMP_MESH_CLK(1);
-    if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); return (double)pl; }
+    if (pl == pl && pl < P - kExactGuard) { TCMP_MESH_STAT(5); TCMP_FA_REC(pl); return (double)pl; }
     if (!inner_first) {
       const float pi = inner_lod();
       TCMP_MESH_CLK(2);
-      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); TCMP_FA_REC(pi); return (double)pi; }
     }
   } else {
     // the mesh's inner box ("collision" above kPen + guard): meshes without LODs, and after the
@@ -1054,7 +1071,7 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     const double* ib = sc.mib + 16 * mi;
     if (ib[12] > 0.0) {
       const float pi = exact_pd_wave32(link, pose(), ib, g);
-      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); return (double)pi; }
+      if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); TCMP_FA_REC(pi); return (double)pi; }
     }
   }
   const HullA32 A{g.verts32, g.planes32, g.eidx, sc.geo_ev, tcmp_geo_vert_off[link],
@@ -1064,14 +1081,16 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
                   rg[20], rg[21]};
   const float pm = hull_hull_wave32<true>(A, B, R, p, P - kExactGuard);
   TCMP_MESH_CLK(3);
-  if (pm == pm && fabsf(pm - P) > kExactGuard) return (double)pm;
+  if (pm == pm && fabsf(pm - P) > kExactGuard) { TCMP_FA_REC(pm); return (double)pm; }
   TCMP_MESH_STAT(7);
   const double r64 = exact_mesh_wave(link, pose_to_lds(), mi, sc.mrange, sc.mp64, sc.mv64, sc.me64,
                                      sc.mcl, g.verts, g.planes, g.edges);
   TCMP_MESH_CLK(4);
+  TCMP_FA_REC(r64);
   return r64;
 #undef TCMP_MESH_STAT
 #undef TCMP_MESH_CLK
+#undef TCMP_FA_REC
 }
 
 // ------------------------------------------------------------------------------------------

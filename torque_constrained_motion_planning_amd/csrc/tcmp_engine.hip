@@ -1812,7 +1812,7 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   TCMP_ENTER(h);
-  if (!out || n < 0 || n > 52) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 84) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   if (int rc_s = sync_stream(h)) return rc_s;
@@ -1826,6 +1826,10 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   HIPCHK(hipMemcpyFromSymbol(ex, HIP_SYMBOL(g_exact_stats), sizeof(ex)));
   for (int i = 0; i < 24 && 12 + i < n && 12 + i < 36; ++i) out[12 + i] = ex[i];
   for (int i = 24; i < 32 && 20 + i < n; ++i) out[20 + i] = ex[i];
+  // 52..83: the mesh chain's head-overlap histogram (g_fa_hist)
+  unsigned long long fh[32];
+  HIPCHK(hipMemcpyFromSymbol(fh, HIP_SYMBOL(g_fa_hist), sizeof(fh)));
+  for (int i = 0; i < 32 && 52 + i < n; ++i) out[52 + i] = fh[i];
 #endif
   return 0;
 }
