@@ -1043,13 +1043,16 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
     TCMP_MESH_CLK(2);
     if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); TCMP_FA_REC(pi); return (double)pi; }
   }
-  const float po = exact_pd_wave32(link, pose(), ob, g);
-  TCMP_MESH_CLK(0);
-  if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); TCMP_FA_REC(po); return (double)po; }
-  // The outer-LOD "free" stage runs only without the sphere certificates: with them, the pairs
-  // that reach the chain are mostly ones the outer LODs cannot prove free (~15 %), and the
-  // full hulls' facet passes prove those anyway -- dropping the stage: C5 edges -10 %, same-box
-  // A/B (profiles/r9g_ab_c5_chain).
+  // The box and outer-LOD stages run only without the sphere certificates: with them, the pairs
+  // that reach the chain are mostly ones those stages cannot decide (the outer LOD proved ~15 %
+  // free, the outer box ~17 %), and the full hulls' facet passes decide them anyway -- without
+  // the outer LOD C5 edges took 10 % less time, without the outer and inner boxes 1 % less
+  // (same-box A/Bs, profiles/r9g_ab_c5_chain, r9j_ab_c5_boxes).
+  if (!inner_first) {
+    const float po = exact_pd_wave32(link, pose(), ob, g);
+    TCMP_MESH_CLK(0);
+    if (po == po && po < P - kExactGuard) { TCMP_MESH_STAT(4); TCMP_FA_REC(po); return (double)po; }
+  }
   if (rg[18] && !inner_first) {
     const HullA32 Ao{sc.lodv3[1], sc.lodpl[1], sc.lodei[1], sc.lodev[1], tcmp_lod_out_vert_off[link],
                      tcmp_lod_out_vert_off[link + 1], tcmp_lod_out_plane_off[link],
@@ -1065,9 +1068,8 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
       TCMP_MESH_CLK(2);
       if (pi == pi && pi > P + kExactGuard) { TCMP_MESH_STAT(6); TCMP_FA_REC(pi); return (double)pi; }
     }
-  } else {
-    // the mesh's inner box ("collision" above kPen + guard): meshes without LODs, and after the
-    // inner LOD with the sphere certificates on (as measured in the A/B above)
+  } else if (!inner_first) {
+    // the mesh's inner box ("collision" above kPen + guard): meshes without LODs
     const double* ib = sc.mib + 16 * mi;
     if (ib[12] > 0.0) {
       const float pi = exact_pd_wave32(link, pose(), ib, g);
