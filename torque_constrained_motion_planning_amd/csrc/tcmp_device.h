@@ -671,6 +671,9 @@ constexpr int max_link_edges() {
 // 2.5 mm doubling to 32 cm, [9] no head, [10] head without an axis) and verdict ([16 + b]
 // collision)
 __device__ unsigned long long g_fa_hist[32];
+// the same pairs by the sphere certificate's best ball-pair overlap (phase B): buckets
+// < -8 cm, -4, -2, -1, 0, 1, 2, 3, 4 cm, [9] no spheres; [16 + b] collision
+__device__ unsigned long long g_sb_hist[32];
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
 __device__ unsigned long long g_exact_stats[32];  // [4..7]: mesh pairs (exact_pair),
@@ -945,7 +948,8 @@ __device__ __forceinline__ float facet_axes_wave(int link, const float R[9], con
 // mesh) -- both hull-vs-box -- then the hull-vs-hull test.  fp32 first, fp64 near kPen.
 template <bool MESH>
 __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const double* ps,
-                                             const double* ob, const Scene sc, const Geo g) {
+                                             const double* ob, const Scene sc, const Geo g,
+                                             float sbest = -INFINITY) {
   const int mi = MESH ? obs_mesh(ob) : -1;
   // mesh kernels: the pose is re-read from the wave's LDS stash (ps: its column, stride 64) at
   // each use instead of living in 24 VGPRs across the hull-vs-hull tests; the clobber keeps
@@ -991,7 +995,12 @@ __device__ __forceinline__ double exact_pair(int link, const Pose PL0, const dou
   const int* rg = sc.mrange + kMrange * mi;
 #ifdef TCMP_PROF_EXACT
   int fab = 9;
-#define TCMP_FA_REC(v) if (lane_id() == 0) atomicAdd(&g_fa_hist[((v) >= kPen ? 16 : 0) + fab], 1ull)
+  const int sbb = !(sbest > -1e30f) ? 9 : sbest < -0.08f ? 0 : sbest < -0.04f ? 1 : sbest < -0.02f ? 2
+                : sbest < -0.01f ? 3 : sbest < 0.f ? 4 : sbest < 0.01f ? 5 : sbest < 0.02f ? 6
+                : sbest < 0.03f ? 7 : 8;
+#define TCMP_FA_REC(v) if (lane_id() == 0) { \
+    atomicAdd(&g_fa_hist[((v) >= kPen ? 16 : 0) + fab], 1ull); \
+    atomicAdd(&g_sb_hist[((v) >= kPen ? 16 : 0) + sbb], 1ull); }
 #else
 #define TCMP_FA_REC(v)
 #endif
@@ -1353,7 +1362,7 @@ __device__ __forceinline__ void link_obb(int link, const double R[9], const doub
 // 1 collision, 2 undecided.  Mesh m: rows TCMP_NSPH * (10 + m) of sph, world frame (link
 // meshes of self pairs: their own link frame, as the pose is then).
 __device__ __forceinline__ int sphere_cert(int link, const float R[9], const float p[3], int mi,
-                                            const Scene sc, const Geo g) {
+                                            const Scene sc, const Geo g, float* bo = nullptr) {
   const float4* LS = sc.csph + TCMP_NSPH * link;               // LDS (mesh kernels)
   const float4* MS = sc.sph + TCMP_NSPH * (TCMP_NLINKS + mi);  // global
   // every mesh ball into the link frame once (u = R^T (t - p)), against the link's balls;
@@ -1375,6 +1384,9 @@ __device__ __forceinline__ int sphere_cert(int link, const float R[9], const flo
       if (ov > best) { best = ov; ax = ex; ay = ey; az = ez; bi = i; bj = j; }
     }
   }
+#ifdef TCMP_PROF_EXACT
+  if (bo) *bo = best;
+#endif
   if (best >= (float)kPen + kExactGuard) return 1;
   const int* rg = sc.mrange + kMrange * mi;
   if (rg[18]) {
@@ -1509,6 +1521,9 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         for (int k = 0; k < 3; ++k) p[k] = pr[k];
       }
       int cls = 0, mi = -1;
+#ifdef TCMP_PROF_EXACT
+      float sbest = -INFINITY;  // the sphere certificate's best ball-pair overlap (prof stats)
+#endif
       bool sat = false;
       if (has) {
         double wc[3], U[9], aabb[3];
@@ -1534,7 +1549,11 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
           for (int k = 0; k < 9; ++k) Rf[k] = (float)ps[k * 64 + lane];
 #pragma unroll
           for (int k = 0; k < 3; ++k) pf[k] = (float)ps[(9 + k) * 64 + lane];
+#ifdef TCMP_PROF_EXACT
+          cls = sphere_cert(lk, Rf, pf, mi, sc, g, &sbest);
+#else
           cls = sphere_cert(lk, Rf, pf, mi, sc, g);
+#endif
 #ifdef TCMP_PROF_EXACT
           if (cls != 2) atomicAdd(&g_exact_stats[cls ? 14 : 15], 1ull);
 #endif
@@ -1564,7 +1583,12 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #ifdef TCMP_PROF
         const unsigned long long te0 = clock64();
 #endif
+#ifdef TCMP_PROF_EXACT
+        const double pd = exact_pair<MESH>(lL, PL, MESH ? stash + 14 * 64 + L : nullptr, ob, sc, g,
+                                           __shfl(sbest, L));
+#else
         const double pd = exact_pair<MESH>(lL, PL, MESH ? stash + 14 * 64 + L : nullptr, ob, sc, g);
+#endif
 #ifdef TCMP_PROF
         st.cyc_exact += clock64() - te0;
 #endif

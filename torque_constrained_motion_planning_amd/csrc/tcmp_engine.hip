@@ -1812,7 +1812,7 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   TCMP_ENTER(h);
-  if (!out || n < 0 || n > 84) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 116) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   if (int rc_s = sync_stream(h)) return rc_s;
@@ -1830,6 +1830,9 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   unsigned long long fh[32];
   HIPCHK(hipMemcpyFromSymbol(fh, HIP_SYMBOL(g_fa_hist), sizeof(fh)));
   for (int i = 0; i < 32 && 52 + i < n; ++i) out[52 + i] = fh[i];
+  // 84..115: the same pairs by the sphere certificate's best overlap (g_sb_hist)
+  HIPCHK(hipMemcpyFromSymbol(fh, HIP_SYMBOL(g_sb_hist), sizeof(fh)));
+  for (int i = 0; i < 32 && 84 + i < n; ++i) out[84 + i] = fh[i];
 #endif
   return 0;
 }
