@@ -20,7 +20,7 @@ def main():
     eng = _lib.Engine(0)
     obs, pack, goal = bench.make_query(1234, n_obs=0, n_mesh=W["meshes"], engine=eng)
     r, _ = bench.run_query(eng, obs, goal, n, W["batch"], 1234, meshes=pack)
-    c = eng.debug_counters(116)
+    c = eng.debug_counters(120)
     tot = max(1, c[0])
     print(json.dumps({"samples": n, "ms_edges": r.ms_edges, "ms_nearest": r.ms_nearest,
                       "edge_steps": r.edge_steps, "pairs_tested": r.pairs_tested,
@@ -45,6 +45,8 @@ def main():
                       "ball_overlap_hist": {"edges_m": [-0.08, -0.04, -0.02, -0.01, 0, 0.01, 0.02,
                                                         0.03, 0.0401, "no spheres"],
                                             "free": c[84:94], "collision": c[100:110]},
+                      "full_stage_clk": {"free_exits": c[116], "collision_facets": c[117],
+                                         "collision_edges": c[118]},
                       "mesh_stage_clk_share": dict(zip(
                           ("outer_box", "outer_lod", "inner_lod", "full_fp32", "fp64"),
                           (round(x / max(1, sum(c[28:33]) + c[46]), 4) for x in c[28:33])))}),

@@ -25,8 +25,13 @@ namespace tcmp {
 
 #ifdef TCMP_PROF_EXACT
 #define TCMP_MSTAT(i) if (lane_id() == 0) atomicAdd(&g_exact_stats[i], 1ull)
+// the full fp32 hull-vs-hull stage's clocks: [0] pairs it proves free, [1] / [2] the facet / edge
+// parts of the pairs that run to the end
+__device__ unsigned long long g_full_clk[4];
+#define TCMP_FCLK(i, t) if (STAT && lane_id() == 0) atomicAdd(&g_full_clk[i], clock64() - (t))
 #else
 #define TCMP_MSTAT(i)
+#define TCMP_FCLK(i, t)
 #endif
 
 // A hull in a link frame (rotated per lane into the world): vertices [V][3], planes (n, d),
@@ -53,6 +58,9 @@ struct HullB32 {
   int c0, c1;
 };
 constexpr int kMaxGaussClusters = 32;
+#ifndef TCMP_REC_UNROLL
+#define TCMP_REC_UNROLL 2  // Gauss records loaded together in the hull-vs-hull edge walk
+#endif
 // slack on the cone test's cosine: far above the fp32 error of the rotated axes (~1e-6), so a
 // pair of arcs that intersect is never pruned
 constexpr float kConeSlack = 2e-3f;
@@ -144,12 +152,18 @@ template <bool STAT>
 __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32 B,
                                                   const float R[9], const float p[3], float stop) {
   const int lane = lane_id();
+#ifdef TCMP_PROF_EXACT
+  const unsigned long long tf0 = clock64();
+#endif
   // (1) B's facets (moved into A's frame) against A's vertices (uniform stream)
   float pd = wave_minf(facets32<true>(A, B, R, p));
-  if (pd < stop) { if (STAT) TCMP_MSTAT(8); return pd; }
+  if (pd < stop) { if (STAT) TCMP_MSTAT(8); TCMP_FCLK(0, tf0); return pd; }
   // (2) A's facets (moved into the world frame) against B's vertices
   pd = fminf(pd, wave_minf(facets32<false>(A, B, R, p)));
-  if (pd < stop) { if (STAT) TCMP_MSTAT(9); return pd; }
+  if (pd < stop) { if (STAT) TCMP_MSTAT(9); TCMP_FCLK(0, tf0); return pd; }
+#ifdef TCMP_PROF_EXACT
+  const unsigned long long te0 = clock64();
+#endif
   float loc = INFINITY;
   // (3) edge pairs whose Gauss-map arcs intersect (Gregorius' Minkowski-face test).  Lanes own
   // A's edges, 64 at a time.  Pass 1: each lane's arc a -> b (A's facet normals in the world) is
@@ -208,9 +222,12 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
           const float cab = na.x * nb.x + na.y * nb.y + na.z * nb.z;
           const float ca = sqrtf(fmaxf(0.f, 0.5f * (1.f + cab))),
                       sa = sqrtf(fmaxf(0.f, 0.5f * (1.f - cab)));
-          const float4* cl = B.cl + 2 * B.c0;
+          // the cluster cones are wave-uniform: scalar loads through the constant address space
+          // (vector loads of one address by every lane were 3 % slower on C5, profiles/r9q_*)
+          cfloat* cl = (cfloat*)(B.cl + 2 * B.c0);
           for (int k = 0; k < nC; ++k) {
-            const float4 c = cl[2 * k], s = cl[2 * k + 1];
+            const float4 c = make_float4(cl[8 * k], cl[8 * k + 1], cl[8 * k + 2], cl[8 * k + 3]);
+            const float4 s = make_float4(cl[8 * k + 4], 0.f, 0.f, 0.f);
             // the cones overlap iff angle(axes) <= half_a + half_b: always when that sum
             // reaches pi (half_b >= pi - half_a, i.e. cos half_b <= -cos half_a; half_a <=
             // pi / 2), else cos(angle) >= cos(half_a + half_b), less the slack
@@ -245,9 +262,10 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
         float ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz;
         a_edge(base + src, ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz);
         const float el2 = ex * ex + ey * ey + ez * ez;
-        for (int k = r0; k < r1; ++k) {
+        // one record: its arc (c -> d) against the lane's edge (Gregorius' test), the axis if
+        // they intersect; r0v / r1v: the record's first 32 bytes, loaded by the caller
+        auto rec = [&](int k, const float4 r0v, const float4 r1v) {
           const float4* E4 = reinterpret_cast<const float4*>(B.er + 16 * k);
-          const float4 r0v = E4[0], r1v = E4[1];  // c (x y z), d (x | y z), w (x y)
           const float cba = r0v.x * ux + r0v.y * uy + r0v.z * uz;
           const float dba = r0v.w * ux + r1v.x * uy + r1v.y * uz;
           if (cba * dba < 0.f) {
@@ -272,14 +290,36 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
               }
             }
           }
+        };
+        // the cluster's records TCMP_REC_UNROLL at a time, their first halves all in flight
+        // before the first test (a record's walk is otherwise one dependent gather at a time)
+        int k = r0;
+#pragma unroll 1
+        for (; k + TCMP_REC_UNROLL <= r1; k += TCMP_REC_UNROLL) {
+          float4 h0[TCMP_REC_UNROLL], h1[TCMP_REC_UNROLL];
+#pragma unroll
+          for (int u = 0; u < TCMP_REC_UNROLL; ++u) {
+            const float4* E4 = reinterpret_cast<const float4*>(B.er + 16 * (k + u));
+            h0[u] = E4[0];
+            h1[u] = E4[1];
+          }
+#pragma unroll
+          for (int u = 0; u < TCMP_REC_UNROLL; ++u) rec(k + u, h0[u], h1[u]);
+        }
+#pragma unroll 1
+        for (; k < r1; ++k) {
+          const float4* E4 = reinterpret_cast<const float4*>(B.er + 16 * k);
+          rec(k, E4[0], E4[1]);
         }
       }
       if ((w0 + 64 < total || base + 64 < A.e1) && !__ballot(deg)) {
         const float lf = fminf(pd, wave_minf(loc));
-        if (lf < stop) { if (STAT) TCMP_MSTAT(10); return lf; }
+        if (lf < stop) { if (STAT) TCMP_MSTAT(10); TCMP_FCLK(0, tf0); return lf; }
       }
     }
   }
+  TCMP_FCLK(1, tf0 + (clock64() - te0));  // the facet part: te0 - tf0
+  TCMP_FCLK(2, te0);
   if (__ballot(deg)) { if (STAT) TCMP_MSTAT(13); return __builtin_nanf(""); }
   const float res = fminf(pd, wave_minf(loc));
   if (STAT) {
@@ -323,10 +363,10 @@ __device__ __noinline__ double exact_mesh_wave(int link, const double* pose, int
     const double nz = R[2] * w.x + R[5] * w.y + R[8] * w.z;
     const double dd = w.w - (w.x * p[0] + w.y * p[1] + w.z * p[2]);
     double mn = INFINITY;
-    for (int v = lv0; v < lv1; ++v) {
-      const double4 P4 = *reinterpret_cast<const double4*>(g.verts + 4 * v);
-      mn = fmin(mn, nx * P4.x + ny * P4.y + nz * P4.z);
-    }
+    typedef const __attribute__((address_space(4))) double cdouble;
+    cdouble* gv = (cdouble*)g.verts;  // wave-uniform stream: scalar loads
+    for (int v = lv0; v < lv1; ++v)
+      mn = fmin(mn, nx * gv[4 * v] + ny * gv[4 * v + 1] + nz * gv[4 * v + 2]);
     loc = fmin(loc, dd - mn);
   }
   double pd = wave_min(loc);
@@ -338,10 +378,10 @@ __device__ __noinline__ double exact_mesh_wave(int link, const double* pose, int
     const double nz = R[6] * W[0] + R[7] * W[1] + R[8] * W[2];
     const double dd = W[3] + (nx * p[0] + ny * p[1] + nz * p[2]);
     double mn = INFINITY;
-    for (int v = v0; v < v1; ++v) {
-      const double4 P4 = sc.mv64[v];
-      mn = fmin(mn, nx * P4.x + ny * P4.y + nz * P4.z);
-    }
+    typedef const __attribute__((address_space(4))) double cdouble;
+    cdouble* mv = (cdouble*)sc.mv64;  // wave-uniform stream: scalar loads
+    for (int v = v0; v < v1; ++v)
+      mn = fmin(mn, nx * mv[4 * v] + ny * mv[4 * v + 1] + nz * mv[4 * v + 2]);
     loc = fmin(loc, dd - mn);
   }
   pd = fmin(pd, wave_min(loc));
