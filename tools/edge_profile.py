@@ -20,11 +20,15 @@ def main():
     eng = _lib.Engine(0)
     obs, _, goal = bench.make_query(1234, engine=eng)
     prev = [0] * 4
+    pprev = [0] * 8
     for q in range(n):
         r, _ = bench.run_query(eng, obs, goal, 1_000_000, 262144, 1234 + q)
-        c = eng.debug_counters(36)
+        c = eng.debug_counters(128)
         ex = [a - b for a, b in zip(c[8:12], prev)]
         prev = c[8:12]
+        ps = [a - b for a, b in zip(c[120:128], pprev)]
+        pprev = c[120:128]
+        npass = max(1, ps[0])
         tot = max(1, c[0])
         print(json.dumps({"query": q, "ms_edges": r.ms_edges, "total_clk": c[0],
                           "fetch": c[1] / tot, "collision": c[2] / tot, "torque": c[3] / tot,
@@ -34,7 +38,15 @@ def main():
                           "exact32_full": ex[2], "exact32_degenerate": ex[3],
                           "edge_steps": r.edge_steps, "pairs_sat": r.pairs_sat,
                           "pairs_exact": r.pairs_exact, "box_cert_collision": c[33],
-                          "box_cert_free": c[34]}), flush=True)
+                          "box_cert_free": c[34],
+                          # phase B's 64-entry passes: entries, distinct source lanes and
+                          # (lane, link) per pass, entries of links 7..9, and the share of
+                          # wave clocks from a pass's start to its exact loop (pose + tiers 1-3)
+                          "phaseB": {"passes": ps[0], "entries_per_pass": ps[1] / npass,
+                                     "lanes_per_pass": ps[2] / npass,
+                                     "lane_links_per_pass": ps[3] / npass,
+                                     "distal_share": ps[4] / max(1, ps[1]),
+                                     "pose_tiers_clk": ps[5] / tot}}), flush=True)
 
 
 if __name__ == "__main__":

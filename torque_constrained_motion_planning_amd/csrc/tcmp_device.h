@@ -676,6 +676,9 @@ __device__ unsigned long long g_fa_hist[32];
 __device__ unsigned long long g_sb_hist[32];
 // exact32 outcomes: [0] box-face exit, [1] facet exit, [2] full or edge-pass exit,
 // [3] degenerate (fp64 fallback)
+// phase-B pass structure: [0] passes, [1] entries, [2] distinct source lanes, [3] distinct
+// (lane, link), [4] entries of links 7..9, [5] clocks from a pass's start to its exact loop
+__device__ unsigned long long g_pass_stats[8];
 __device__ unsigned long long g_exact_stats[32];  // [4..7]: mesh pairs (exact_pair),
                                                   // [8..13]: hull_hull_wave32 exits,
                                                   // [16..20]: exact_pair mesh-stage clocks
@@ -1520,6 +1523,28 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #pragma unroll
         for (int k = 0; k < 3; ++k) p[k] = pr[k];
       }
+#ifdef TCMP_PROF_EXACT
+      const unsigned long long tp0 = clock64();
+      {
+        unsigned dl = 0, dl2 = 0, dlk = 0;
+        const unsigned sb = has ? 1u << (src & 31) : 0u;
+        dl = __popc(wave_or_u32(src < 32 ? sb : 0u)) + __popc(wave_or_u32(src >= 32 ? sb : 0u));
+        for (int l = 0; l < 10; ++l) {
+          const bool on = has && lk == l;
+          dlk += __popc(wave_or_u32(on && src < 32 ? sb : 0u)) +
+                 __popc(wave_or_u32(on && src >= 32 ? sb : 0u));
+        }
+        dl2 = (unsigned)__popcll(__ballot(has && lk >= 7));
+        const unsigned long long ne = __popcll(__ballot(has));
+        if (lane == 0) {
+          atomicAdd(&g_pass_stats[0], 1ull);
+          atomicAdd(&g_pass_stats[1], ne);
+          atomicAdd(&g_pass_stats[2], (unsigned long long)dl);
+          atomicAdd(&g_pass_stats[3], (unsigned long long)dlk);
+          atomicAdd(&g_pass_stats[4], (unsigned long long)dl2);
+        }
+      }
+#endif
       int cls = 0, mi = -1;
 #ifdef TCMP_PROF_EXACT
       float sbest = -INFINITY;  // the sphere certificate's best ball-pair overlap (prof stats)
@@ -1562,6 +1587,9 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       st.pairs_sat += (unsigned)__popcll(__ballot(sat));
       if (cls == 1) atomicOr(cmask, 1ull << src);
       uint64_t pend = __ballot(cls == 2);
+#ifdef TCMP_PROF_EXACT
+      if (lane == 0) atomicAdd(&g_pass_stats[5], clock64() - tp0);
+#endif
       while (pend) {
         const int L = __builtin_ctzll(pend);
         pend &= pend - 1;

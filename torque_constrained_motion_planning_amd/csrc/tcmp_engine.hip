@@ -1812,7 +1812,7 @@ int tcmp_version(void) { return 1; }
 
 int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   TCMP_ENTER(h);
-  if (!out || n < 0 || n > 120) return fail(-1, "bad arguments");
+  if (!out || n < 0 || n > 128) return fail(-1, "bad arguments");
   DevState s;
   HIPCHK(hipMemcpyAsync(&s, h->st, sizeof(s), hipMemcpyDeviceToHost, h->stream));
   if (int rc_s = sync_stream(h)) return rc_s;
@@ -1836,6 +1836,9 @@ int tcmp_debug_counters(tcmp_handle* h, uint64_t* out, int32_t n) {
   // 116..119: the full fp32 stage's clocks (g_full_clk)
   HIPCHK(hipMemcpyFromSymbol(fh, HIP_SYMBOL(g_full_clk), 4 * sizeof(unsigned long long)));
   for (int i = 0; i < 4 && 116 + i < n; ++i) out[116 + i] = fh[i];
+  // 120..127: phase B's pass structure (g_pass_stats)
+  HIPCHK(hipMemcpyFromSymbol(fh, HIP_SYMBOL(g_pass_stats), 8 * sizeof(unsigned long long)));
+  for (int i = 0; i < 8 && 120 + i < n; ++i) out[120 + i] = fh[i];
 #endif
   return 0;
 }

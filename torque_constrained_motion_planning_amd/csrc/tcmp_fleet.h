@@ -259,8 +259,14 @@ __global__ __launch_bounds__(256) void k_fl_edge_records(const FleetPlan* __rest
 // wave starts at plan (its index * K / waves); when that plan's queue is empty and its lanes
 // have finished, it posts its counts to the plan and takes the next plan, until it has been
 // through all K.  nb: the round's edge count (every plan's).
+// behind the lanes' last safe configurations, their edges' targets ([7][512] doubles, written
+// at fetch) when the fleet's LDS has room for them (C3 fleets of four; not C4's sixteen): the
+// two target reads per step are LDS reads instead of L2 round trips, k_fl_edges 3.152 -> 3.118 ms
+// per C3 launch (same-box A/B, profiles/r9w_ab_fetch/; reserving 16 work slots per counter
+// atomic instead of a step's need measured no change and is not kept)
+__host__ __device__ constexpr unsigned fleet_q2_bytes() { return 7u * 512u * sizeof(double); }
 __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict__ fp, int K, int nb,
-                                                     Geo g_g) {
+                                                     Geo g_g, int q2lds) {
   extern __shared__ double tcmp_lds[];
   Scene s0{};
   Geo g;
@@ -293,6 +299,16 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
 #pragma unroll
     for (int k = 0; k < 7; ++k) qcol[512 * k] = o[k];
   };
+  // the edge's target: its LDS column behind qcol's (written at fetch) or global memory
+  double* const tcol = qcol + 7 * 512;
+  auto get_t = [&](double o[7]) {
+    if (q2lds) {
+#pragma unroll
+      for (int k = 0; k < 7; ++k) o[k] = tcol[512 * k];
+    } else {
+      load7(F->J.to + 8 * (size_t)e, o);
+    }
+  };
   {
     const double mid[7] = {0.5 * (kLo[0] + kHi[0]), 0.5 * (kLo[1] + kHi[1]), 0.5 * (kLo[2] + kHi[2]),
                            0.5 * (kLo[3] + kHi[3]), 0.5 * (kLo[4] + kHi[4]), 0.5 * (kLo[5] + kHi[5]),
@@ -314,12 +330,18 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
         if (my < nb) {
           const double* rec = F->J.rec + 8 * (size_t)my;
           const double4 ra = *reinterpret_cast<const double4*>(rec);
-          const double4 rb = *reinterpret_cast<const double4*>(rec + 4);
-          const double qf[7] = {ra.x, ra.y, ra.z, ra.w, rb.x, rb.y, rb.z};
+          const double4 rb4 = *reinterpret_cast<const double4*>(rec + 4);
+          const double qf[7] = {ra.x, ra.y, ra.z, ra.w, rb4.x, rb4.y, rb4.z};
           put_q(qf);
-          e = __double2loint(rb.w);
-          n = __double2hiint(rb.w);
+          e = __double2loint(rb4.w);
+          n = __double2hiint(rb4.w);
           i = 0;
+          if (q2lds) {
+            double q2[7];
+            load7(F->J.to + 8 * (size_t)e, q2);
+#pragma unroll
+            for (int k = 0; k < 7; ++k) tcol[512 * k] = q2[k];
+          }
         } else {
           done = true;
         }
@@ -349,7 +371,7 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
       double qn[7], q2[7];
       get_q(qn);
       if (active) {
-        load7(F->J.to + 8 * (size_t)e, q2);
+        get_t(q2);
         refine_step(qn, q2, n, i);
       }
 #pragma unroll
@@ -375,7 +397,7 @@ __global__ __launch_bounds__(512, 1) void k_fl_edges(const FleetPlan* __restrict
       get_q(qc);
       if (ok) {
         double q2[7];
-        load7(F->J.to + 8 * (size_t)e, q2);
+        get_t(q2);
         refine_step(qc, q2, n, i);
         put_q(qc);
         ++i;
@@ -651,8 +673,11 @@ int fleet_round(const Fleet& F, int nb, long long base) {
                        lds_bytes(h), h->stream, F.fp, K, nb, h->scene(), h->geo());
   } else {
     const long long blocks = std::min<long long>(h->cu_count, ((long long)K * nb + 511) / 512);
+    const unsigned lds = fleet_lds_bytes(F.lds_obs);
+    const int q2lds = lds + fleet_q2_bytes() <= kFleetLdsCap;
     hipLaunchKernelGGL(k_fl_edges, dim3((unsigned)std::max<long long>(1, blocks)), dim3(512),
-                       fleet_lds_bytes(F.lds_obs), h->stream, F.fp, K, nb, h->geo());
+                       lds + (q2lds ? fleet_q2_bytes() : 0u), h->stream, F.fp, K, nb, h->geo(),
+                       q2lds);
   }
   HIPCHK(hipGetLastError());
   const hipEvent_t ee = h->mark_end(F_EDGES, ek);
