@@ -1129,6 +1129,27 @@ struct StepStats {
 #endif
 };
 
+// Products with a compile-time zero factor are skipped (the joint rotations' and offsets' zero
+// entries, the identity rotations of the flange and finger frames): x * 0 adds a signed zero, so
+// for finite operands the sums are the full expressions' up to the sign of a zero result.
+// (Multiplication by a constant 1 the compiler folds itself.)
+__device__ __forceinline__ bool zconst(double k) { return __builtin_constant_p(k) && k == 0.0; }
+__device__ __forceinline__ double zmul(double a, double b) {
+  return (zconst(a) || zconst(b)) ? 0.0 : a * b;
+}
+__device__ __forceinline__ double zdot3(double a0, double b0, double a1, double b1, double a2,
+                                        double b2) {
+  const bool z0 = zconst(a0) || zconst(b0), z1 = zconst(a1) || zconst(b1),
+             z2 = zconst(a2) || zconst(b2);
+  if (z0 && z1 && z2) return 0.0;
+  if (z0 && z1) return a2 * b2;
+  if (z0 && z2) return a1 * b1;
+  if (z1 && z2) return a0 * b0;
+  if (z0) return a1 * b1 + a2 * b2;
+  if (z1) return a0 * b0 + a2 * b2;
+  if (z2) return a0 * b0 + a1 * b1;
+  return a0 * b0 + a1 * b1 + a2 * b2;
+}
 __device__ __forceinline__ void frame_step(double R[9], double p[3], const double Rl[9],
                                            const double t[3]) {
   double nR[9], np[3];
@@ -1136,8 +1157,8 @@ __device__ __forceinline__ void frame_step(double R[9], double p[3], const doubl
   for (int i = 0; i < 3; ++i) {
 #pragma unroll
     for (int j = 0; j < 3; ++j)
-      nR[3 * i + j] = R[3 * i + 0] * Rl[0 + j] + R[3 * i + 1] * Rl[3 + j] + R[3 * i + 2] * Rl[6 + j];
-    np[i] = R[3 * i + 0] * t[0] + R[3 * i + 1] * t[1] + R[3 * i + 2] * t[2] + p[i];
+      nR[3 * i + j] = zdot3(R[3 * i + 0], Rl[0 + j], R[3 * i + 1], Rl[3 + j], R[3 * i + 2], Rl[6 + j]);
+    np[i] = zdot3(R[3 * i + 0], t[0], R[3 * i + 1], t[1], R[3 * i + 2], t[2]) + p[i];
   }
 #pragma unroll
   for (int k = 0; k < 9; ++k) R[k] = nR[k];
@@ -1163,7 +1184,7 @@ __device__ __forceinline__ bool torque_ok_dyn(const double cq[7], const double s
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
-    const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+    const double Rl[9] = {c, -s, 0.0, zmul(cr, s), zmul(cr, c), -sr, zmul(sr, s), zmul(sr, c), cr};
     const double t[3] = {kJx[j], kJy[j], kJz[j]};
     frame_step(R, p, Rl, t);
     zx[j] = R[2];
@@ -1284,6 +1305,17 @@ __device__ constexpr int kSelfB[kNumSelfPairs] = {
     2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6,
     7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9};
 
+// tier 0's boxes of the hand and the two fingers (collision links 7..9) in their own frames:
+// centre, half extents of their hull vertices (panda_geometry.npz verts; the fp64 min / max,
+// so the box holds the hull up to ~1e-17 m, inside tier 0's 1e-5 margin)
+constexpr double kT0Box[3][6] = {
+    {-1.0067597031593323e-05, -0.0017819218337535858, 0.020018674433231354,
+     0.03162585012614727, 0.10220779851078987, 0.045943476259708405},
+    {7.68294557929039e-06, 0.013135369845258538, 0.02699036512785824,
+     0.010487135965377092, 0.013268012575281318, 0.026858668883505743},
+    {-7.682945576062937e-06, -0.013135369845260508, 0.02699036512785824,
+     0.010487135965377196, 0.013268012575281492, 0.026858668883505743}};
+
 // Returns collision flag; all lanes must call.  `active` lanes only contribute.
 //
 // Phase A (every step): the 10 link frames are generated incrementally and each link's world
@@ -1303,7 +1335,7 @@ __device__ __forceinline__ void link_pose(int link, const double cq[7], const do
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
-    const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+    const double Rl[9] = {c, -s, 0.0, zmul(cr, s), zmul(cr, c), -sr, zmul(sr, s), zmul(sr, c), cr};
     const double t[3] = {kJx[j], kJy[j], kJz[j]};
     frame_step(R, p, Rl, t);
     if (j == link) {
@@ -1640,8 +1672,20 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
     float bc[10][3], bh[10][3];
     {
       auto put = [&](int link, const double Rr[9], const double pr[3]) {
-        double wc[3], U[9], aabb[3];
-        link_obb(link, Rr, pr, wc, U, aabb);
+        double wc[3], aabb[3];
+        if (link >= 7) {
+          // the hand and fingers: their hulls' boxes in their own frames (U = R: no axis
+          // products; as tight as their OBBs, which are within 4 degrees of the frame axes)
+          const double* b = kT0Box[link - 7];
+#pragma unroll
+          for (int i = 0; i < 3; ++i) {
+            wc[i] = Rr[3 * i + 0] * b[0] + Rr[3 * i + 1] * b[1] + Rr[3 * i + 2] * b[2] + pr[i];
+            aabb[i] = b[3] * fabs(Rr[3 * i + 0]) + b[4] * fabs(Rr[3 * i + 1]) + b[5] * fabs(Rr[3 * i + 2]);
+          }
+        } else {
+          double U[9];
+          link_obb(link, Rr, pr, wc, U, aabb);
+        }
 #pragma unroll
         for (int i = 0; i < 3; ++i) {
           bc[link][i] = (float)wc[i];
@@ -1651,9 +1695,15 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
       double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
 #pragma unroll
       for (int j = 0; j < 7; ++j) {
-        const double cr = kJcr[j], sr = kJsr[j], c = MESH ? stash[j * 64 + lane] : cq[j],
+        // (the joints' cos(alpha) = kCr = 4.9e-12 as an exact 0 here, which drops a third of
+        // each frame step's products: the frames move by < 1e-10 m, far inside the boxes'
+        // 1e-5 margin; phase B and the exact tests keep kCr.  With the hand boxes below and
+        // the zero-skipping frame steps: k_fl_edges 3.13 -> 3.10 ms per C3 launch, same-box
+        // A/B, profiles/r9z_ab_tier0/)
+        const double cr = j > 0 ? 0.0 : kJcr[j], sr = kJsr[j],
+                     c = MESH ? stash[j * 64 + lane] : cq[j],
                      s = MESH ? stash[(7 + j) * 64 + lane] : sq[j];
-        const double Rl[9] = {c, -s, 0.0, cr * s, cr * c, -sr, sr * s, sr * c, cr};
+        const double Rl[9] = {c, -s, 0.0, zmul(cr, s), zmul(cr, c), -sr, zmul(sr, s), zmul(sr, c), cr};
         const double t[3] = {kJx[j], kJy[j], kJz[j]};
         frame_step(R, p, Rl, t);
         put(j, R, p);
