@@ -29,3 +29,18 @@ def engine_with_split(split):
             os.environ.pop("TCMP_EDGE_SPLIT", None)
         else:
             os.environ["TCMP_EDGE_SPLIT"] = old
+
+
+@pytest.fixture(autouse=True)
+def _oracle_state_reset():
+    """The oracle library's scene state (installed convex meshes, self-collision switch) is
+    module-level: a test that installs it (e.g. bench.py's C5 sub-line on the CPU fake engine)
+    must not leak it into the next one."""
+    yield
+    if "oracle" in sys.modules:
+        O = sys.modules["oracle"]
+        try:
+            O.set_meshes(None)
+            O.set_self_collision(False)
+        except OSError:  # the library never loaded
+            pass
