@@ -57,7 +57,11 @@ struct HullB32 {
   const float4* cl;
   int c0, c1;
 };
-constexpr int kMaxGaussClusters = 32;
+#ifndef TCMP_GAUSS_CL
+#define TCMP_GAUSS_CL 128  // Gauss-map clusters per hull at most (<= 128: two mask words)
+#endif
+constexpr int kMaxGaussClusters = TCMP_GAUSS_CL;
+static_assert(kMaxGaussClusters <= 128, "cluster masks: two 64-bit words");
 #ifndef TCMP_REC_UNROLL
 #define TCMP_REC_UNROLL 2  // Gauss records loaded together in the hull-vs-hull edge walk
 #endif
@@ -203,7 +207,8 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
       py = R[3] * x0 + R[4] * y0 + R[5] * z0 + p[1];
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
     };
-    unsigned cm = 0;  // pass 1: bit k = cluster c0 + k may hold an arc crossing this lane's
+    // pass 1: bit k of (cm0, cm1) = cluster c0 + k may hold an arc crossing this lane's
+    unsigned long long cm0 = 0, cm1 = 0;
     {
       const int e = base + lane;
       if (e < A.e1) {
@@ -213,7 +218,9 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
         const float sx = na.x + nb.x, sy = na.y + nb.y, sz = na.z + nb.z;
         const float s2 = sx * sx + sy * sy + sz * sz;
         if (!(s2 > 1e-6f)) {
-          cm = nC >= 32 ? 0xffffffffu : ((1u << nC) - 1u);  // a knife edge: no cone
+          // a knife edge: no cone, every cluster
+          cm0 = nC >= 64 ? ~0ull : ((1ull << nC) - 1);
+          if (kMaxGaussClusters > 64 && nC > 64) cm1 = nC >= 128 ? ~0ull : ((1ull << (nC - 64)) - 1);
         } else {
           const float is = rsqrtf(s2);
           const float qx = (R[0] * sx + R[1] * sy + R[2] * sz) * is;
@@ -233,12 +240,15 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
             // pi / 2), else cos(angle) >= cos(half_a + half_b), less the slack
             if (c.w <= -ca + kConeSlack ||
                 qx * c.x + qy * c.y + qz * c.z >= ca * c.w - sa * s.x - kConeSlack)
-              cm |= 1u << k;
+            {
+              if (kMaxGaussClusters > 64 && k >= 64) cm1 |= 1ull << (k - 64);
+              else cm0 |= 1ull << k;
+            }
           }
         }
       }
     }
-    const int cnt = __builtin_popcount(cm);
+    const int cnt = __popcll(cm0) + (kMaxGaussClusters > 64 ? __popcll(cm1) : 0);
     int pre = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -253,11 +263,17 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
 #pragma unroll
       for (int step = 32; step; step >>= 1)
         if (__shfl(pre, src + step) <= w) src += step;
-      unsigned m = (unsigned)__shfl((int)cm, src);
-      const int kk = w - __shfl(pre, src);
+      unsigned long long m = (unsigned long long)__shfl((long long)cm0, src);
+      unsigned long long m1 = kMaxGaussClusters > 64 ? (unsigned long long)__shfl((long long)cm1, src) : 0ull;
+      int kk = w - __shfl(pre, src);
       if (w < total) {
+        int cbase = 0;
+        if (kMaxGaussClusters > 64) {
+          const int c0n = __popcll(m);
+          if (kk >= c0n) { kk -= c0n; m = m1; cbase = 64; }
+        }
         for (int j = 0; j < kk; ++j) m &= m - 1;
-        const float4 cs = B.cl[2 * (B.c0 + __builtin_ctz(m)) + 1];
+        const float4 cs = B.cl[2 * (B.c0 + cbase + __builtin_ctzll(m)) + 1];
         const int r0 = __float_as_int(cs.y), r1 = __float_as_int(cs.z);
         float ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz;
         a_edge(base + src, ax, ay, az, bx, by, bz, ux, uy, uz, ex, ey, ez, px, py, pz);
