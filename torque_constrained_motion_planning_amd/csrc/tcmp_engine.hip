@@ -2068,11 +2068,12 @@ void edge_records(const double* verts, const int32_t* vert_off, const double* pl
 // (angle to an arc's axis + that arc's half-angle), plus 1e-3 rad.  Returns the clusters'
 // index range in cl through c0 / c1.  Record order does not matter anywhere else (every
 // consumer takes a minimum over all records).
-// (at most 128 clusters of at least 3 records: C5 11.15M -> 12.05M samples/s against 32 of at
+// (at most 128 clusters of at least 2 records: C5 11.15M -> 12.05M samples/s against 32 of at
 // least 8, k_fl_edges_mesh 61.1 -> 55.9 ms per launch, same-box A/B, profiles/r9zj_ab_c5_clusters/:
-// the pass-2 walks shrink faster than the pass-1 cone tests grow)
+// the pass-2 walks shrink faster than the pass-1 cone tests grow; >= 2 records another 0.5 %,
+// 192 / 256 clusters slower, profiles/r9zk_ab_c5_clusters/)
 #ifndef TCMP_GAUSS_MINREC
-#define TCMP_GAUSS_MINREC 3  // records per cluster at least
+#define TCMP_GAUSS_MINREC 2  // records per cluster at least
 #endif
 void gauss_clusters(double* rec, int e0, int e1, std::vector<float>& cl, int* c0, int* c1) {
   const int n = e1 - e0;

@@ -61,7 +61,8 @@ struct HullB32 {
 #define TCMP_GAUSS_CL 128  // Gauss-map clusters per hull at most (<= 128: two mask words)
 #endif
 constexpr int kMaxGaussClusters = TCMP_GAUSS_CL;
-static_assert(kMaxGaussClusters <= 128, "cluster masks: two 64-bit words");
+constexpr int kClWords = (kMaxGaussClusters + 63) / 64;  // 64-bit candidate mask words per lane
+static_assert(kClWords <= 4, "cluster masks: at most four 64-bit words");
 #ifndef TCMP_REC_UNROLL
 #define TCMP_REC_UNROLL 2  // Gauss records loaded together in the hull-vs-hull edge walk
 #endif
@@ -207,8 +208,10 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
       py = R[3] * x0 + R[4] * y0 + R[5] * z0 + p[1];
       pz = R[6] * x0 + R[7] * y0 + R[8] * z0 + p[2];
     };
-    // pass 1: bit k of (cm0, cm1) = cluster c0 + k may hold an arc crossing this lane's
-    unsigned long long cm0 = 0, cm1 = 0;
+    // pass 1: bit k of cm[k / 64] = cluster c0 + k may hold an arc crossing this lane's
+    unsigned long long cm[kClWords];
+#pragma unroll
+    for (int w = 0; w < kClWords; ++w) cm[w] = 0;
     {
       const int e = base + lane;
       if (e < A.e1) {
@@ -219,8 +222,11 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
         const float s2 = sx * sx + sy * sy + sz * sz;
         if (!(s2 > 1e-6f)) {
           // a knife edge: no cone, every cluster
-          cm0 = nC >= 64 ? ~0ull : ((1ull << nC) - 1);
-          if (kMaxGaussClusters > 64 && nC > 64) cm1 = nC >= 128 ? ~0ull : ((1ull << (nC - 64)) - 1);
+#pragma unroll
+          for (int w = 0; w < kClWords; ++w) {
+            const int r = nC - 64 * w;
+            cm[w] = r >= 64 ? ~0ull : r > 0 ? ((1ull << r) - 1) : 0ull;
+          }
         } else {
           const float is = rsqrtf(s2);
           const float qx = (R[0] * sx + R[1] * sy + R[2] * sz) * is;
@@ -232,23 +238,27 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
           // the cluster cones are wave-uniform: scalar loads through the constant address space
           // (vector loads of one address by every lane were 3 % slower on C5, profiles/r9q_*)
           cfloat* cl = (cfloat*)(B.cl + 2 * B.c0);
-          for (int k = 0; k < nC; ++k) {
-            const float4 c = make_float4(cl[8 * k], cl[8 * k + 1], cl[8 * k + 2], cl[8 * k + 3]);
-            const float4 s = make_float4(cl[8 * k + 4], 0.f, 0.f, 0.f);
-            // the cones overlap iff angle(axes) <= half_a + half_b: always when that sum
-            // reaches pi (half_b >= pi - half_a, i.e. cos half_b <= -cos half_a; half_a <=
-            // pi / 2), else cos(angle) >= cos(half_a + half_b), less the slack
-            if (c.w <= -ca + kConeSlack ||
-                qx * c.x + qy * c.y + qz * c.z >= ca * c.w - sa * s.x - kConeSlack)
-            {
-              if (kMaxGaussClusters > 64 && k >= 64) cm1 |= 1ull << (k - 64);
-              else cm0 |= 1ull << k;
+#pragma unroll
+          for (int w = 0; w < kClWords; ++w) {
+            unsigned long long bits = 0;
+            for (int k = 64 * w; k < min(nC, 64 * w + 64); ++k) {
+              const float4 c = make_float4(cl[8 * k], cl[8 * k + 1], cl[8 * k + 2], cl[8 * k + 3]);
+              const float4 s = make_float4(cl[8 * k + 4], 0.f, 0.f, 0.f);
+              // the cones overlap iff angle(axes) <= half_a + half_b: always when that sum
+              // reaches pi (half_b >= pi - half_a, i.e. cos half_b <= -cos half_a; half_a <=
+              // pi / 2), else cos(angle) >= cos(half_a + half_b), less the slack
+              if (c.w <= -ca + kConeSlack ||
+                  qx * c.x + qy * c.y + qz * c.z >= ca * c.w - sa * s.x - kConeSlack)
+                bits |= 1ull << (k - 64 * w);
             }
+            cm[w] = bits;
           }
         }
       }
     }
-    const int cnt = __popcll(cm0) + (kMaxGaussClusters > 64 ? __popcll(cm1) : 0);
+    int cnt = 0;
+#pragma unroll
+    for (int w = 0; w < kClWords; ++w) cnt += __popcll(cm[w]);
     int pre = cnt;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -263,14 +273,22 @@ __device__ __forceinline__ float hull_hull_wave32(const HullA32 A, const HullB32
 #pragma unroll
       for (int step = 32; step; step >>= 1)
         if (__shfl(pre, src + step) <= w) src += step;
-      unsigned long long m = (unsigned long long)__shfl((long long)cm0, src);
-      unsigned long long m1 = kMaxGaussClusters > 64 ? (unsigned long long)__shfl((long long)cm1, src) : 0ull;
+      unsigned long long mw[kClWords];
+#pragma unroll
+      for (int x = 0; x < kClWords; ++x) mw[x] = (unsigned long long)__shfl((long long)cm[x], src);
       int kk = w - __shfl(pre, src);
       if (w < total) {
+        // the kk-th candidate of lane src: its word, then its bit
+        unsigned long long m = mw[0];
         int cbase = 0;
-        if (kMaxGaussClusters > 64) {
-          const int c0n = __popcll(m);
-          if (kk >= c0n) { kk -= c0n; m = m1; cbase = 64; }
+        bool found = false;
+#pragma unroll
+        for (int x = 0; x < kClWords; ++x) {
+          const int n = __popcll(mw[x]);
+          if (!found) {
+            if (kk < n) { m = mw[x]; cbase = 64 * x; found = true; }
+            else kk -= n;
+          }
         }
         for (int j = 0; j < kk; ++j) m &= m - 1;
         const float4 cs = B.cl[2 * (B.c0 + cbase + __builtin_ctzll(m)) + 1];
