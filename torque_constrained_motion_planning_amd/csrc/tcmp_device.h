@@ -1150,6 +1150,21 @@ __device__ __forceinline__ double zdot3(double a0, double b0, double a1, double 
   if (z2) return a0 * b0 + a1 * b1;
   return a0 * b0 + a1 * b1 + a2 * b2;
 }
+__device__ __forceinline__ void frame_step_full(double R[9], double p[3], const double Rl[9],
+                                                const double t[3]) {
+  double nR[9], np[3];
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+      nR[3 * i + j] = R[3 * i + 0] * Rl[0 + j] + R[3 * i + 1] * Rl[3 + j] + R[3 * i + 2] * Rl[6 + j];
+    np[i] = R[3 * i + 0] * t[0] + R[3 * i + 1] * t[1] + R[3 * i + 2] * t[2] + p[i];
+  }
+#pragma unroll
+  for (int k = 0; k < 9; ++k) R[k] = nR[k];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) p[k] = np[k];
+}
 __device__ __forceinline__ void frame_step(double R[9], double p[3], const double Rl[9],
                                            const double t[3]) {
   double nR[9], np[3];
@@ -1329,15 +1344,22 @@ constexpr double kT0Box[3][6] = {
 // wave-cooperative exact test (fp32 first pass, fp64 when near kPen or degenerate).
 // Tiers 0-3 are conservative bounds of the exact test, so the answer is the exact test's.
 // world frame of `link` (0..9) as collides_wave's phase A builds it, for per-lane links
+// FULL: the frame steps without the zero-skipping (the box kernels' phase B: the same values,
+// and their register allocation spills 16 B per lane instead of 64; the mesh kernels' the
+// other way round, 80 B instead of 144)
+template <bool FULL = false>
 __device__ __forceinline__ void link_pose(int link, const double cq[7], const double sq[7],
                                           double Ro[9], double po[3]) {
+  auto fstep = [](double R[9], double p[3], const double Rl[9], const double t[3]) {
+    if (FULL) frame_step_full(R, p, Rl, t); else frame_step(R, p, Rl, t);
+  };
   double R[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1}, p[3] = {0, 0, 0};
 #pragma unroll
   for (int j = 0; j < 7; ++j) {
     const double cr = kJcr[j], sr = kJsr[j], c = cq[j], s = sq[j];
     const double Rl[9] = {c, -s, 0.0, zmul(cr, s), zmul(cr, c), -sr, zmul(sr, s), zmul(sr, c), cr};
     const double t[3] = {kJx[j], kJy[j], kJz[j]};
-    frame_step(R, p, Rl, t);
+    fstep(R, p, Rl, t);
     if (j == link) {
 #pragma unroll
       for (int k = 0; k < 9; ++k) Ro[k] = R[k];
@@ -1347,13 +1369,13 @@ __device__ __forceinline__ void link_pose(int link, const double cq[7], const do
   }
   const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
   const double tz[3] = {0, 0, kFlangeZ};
-  frame_step(R, p, I, tz);
+  fstep(R, p, I, tz);
   const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
   const double z0[3] = {0, 0, 0};
-  frame_step(R, p, Rz, z0);
+  fstep(R, p, Rz, z0);
   if (link >= 7) {
     const double tf[3] = {0, link == 8 ? kFingerOpen : -kFingerOpen, kFingerZ};
-    if (link > 7) frame_step(R, p, I, tf);
+    if (link > 7) fstep(R, p, I, tf);
 #pragma unroll
     for (int k = 0; k < 9; ++k) Ro[k] = R[k];
 #pragma unroll
@@ -1533,7 +1555,7 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
         s[k] = sq_of(k, src);
       }
       double R[9], p[3];
-      link_pose(lk, c, s, R, p);
+      link_pose<!MESH>(lk, c, s, R, p);
       // obstacle record row: the obstacle, or for a self pair the other link's outer box in
       // its own frame (row n_obs + j) -- the pose then becomes lk's pose in link j's frame
       int orow = o;
