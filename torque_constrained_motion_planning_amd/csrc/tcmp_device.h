@@ -1320,6 +1320,10 @@ __device__ constexpr int kSelfB[kNumSelfPairs] = {
     2, 3, 4, 5, 6, 3, 4, 5, 6, 4, 5, 6, 5, 6, 6,
     7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9, 7, 8, 9};
 
+// phase A's frame steps: zero-skipping in the box kernels, plain in the mesh kernels (the same
+// values; the mesh kernels' register allocation spills 48 B per lane with the plain steps
+// against 80 B, at the same speed, profiles/r9zr_ab_c5_frames/)
+#define TCMP_FSA(...) (MESH ? frame_step_full(__VA_ARGS__) : frame_step(__VA_ARGS__))
 // tier 0's boxes of the hand and the two fingers (collision links 7..9) in their own frames:
 // centre, half extents of their hull vertices (panda_geometry.npz verts; the fp64 min / max,
 // so the box holds the hull up to ~1e-17 m, inside tier 0's 1e-5 margin)
@@ -1727,15 +1731,15 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
                      s = MESH ? stash[(7 + j) * 64 + lane] : sq[j];
         const double Rl[9] = {c, -s, 0.0, zmul(cr, s), zmul(cr, c), -sr, zmul(sr, s), zmul(sr, c), cr};
         const double t[3] = {kJx[j], kJy[j], kJz[j]};
-        frame_step(R, p, Rl, t);
+        TCMP_FSA(R, p, Rl, t);
         put(j, R, p);
       }
       const double I[9] = {1, 0, 0, 0, 1, 0, 0, 0, 1};
       const double tz[3] = {0, 0, kFlangeZ};
-      frame_step(R, p, I, tz);
+      TCMP_FSA(R, p, I, tz);
       const double Rz[9] = {kHandCy, -kHandSy, 0, kHandSy, kHandCy, 0, 0, 0, 1};
       const double z0[3] = {0, 0, 0};
-      frame_step(R, p, Rz, z0);
+      TCMP_FSA(R, p, Rz, z0);
       put(7, R, p);
       double Rf[9], pf[3];
 #pragma unroll
@@ -1743,10 +1747,10 @@ __device__ __forceinline__ bool collides_wave(const double cq[7], const double s
 #pragma unroll
       for (int k = 0; k < 3; ++k) pf[k] = p[k];
       const double tl[3] = {0, kFingerOpen, kFingerZ};
-      frame_step(Rf, pf, I, tl);
+      TCMP_FSA(Rf, pf, I, tl);
       put(8, Rf, pf);
       const double tr[3] = {0, -kFingerOpen, kFingerZ};
-      frame_step(R, p, I, tr);
+      TCMP_FSA(R, p, I, tr);
       put(9, R, p);
     }
     // self pairs whose link AABBs overlap by kPen on all three axes (tier 0 of a self pair;
